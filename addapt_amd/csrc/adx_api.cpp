@@ -1,0 +1,1012 @@
+// C ABI of the MI355X engine (include/addapt_gpu.h): run setup on the host,
+// device buffers, kernel launches.  The reference's objects this replaces are
+// cited per function; the heavy lifting is in kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/addapt_gpu.h"
+#include "dev_types.hpp"
+#include "energy.hpp"
+
+namespace adx {
+size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
+hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
+                        double *terms, float *dG, hipStream_t stream);
+hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream);
+constexpr int NT = 512;
+constexpr size_t LDS_MAX = 163840;
+}  // namespace adx
+
+using namespace adx;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static adx_status fail(adx_status s, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(ADX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
+    } while (0)
+
+extern "C" const char *adx_last_error(void) { return g_err.c_str(); }
+extern "C" int adx_abi_version(void) { return ADX_ABI_VERSION; }
+extern "C" double adx_kT(void) { return kT_kcal(); }
+
+// ------------------------------------------------------------------ params
+struct adx_params {
+    EnergyParams P;
+};
+
+extern "C" adx_status adx_params_load(const char *path, adx_params **out) {
+    if (!path || !out) return fail(ADX_EINVAL, "adx_params_load: null argument");
+    auto p = std::make_unique<adx_params>();
+    std::string err;
+    if (!load_params(path, p->P, err)) return fail(ADX_EPARAM, "%s", err.c_str());
+    *out = p.release();
+    return ADX_OK;
+}
+
+extern "C" void adx_params_free(adx_params *p) { delete p; }
+
+extern "C" adx_status adx_eval_structure(const adx_params *p, const char *seq, const char *st,
+                                         double *e) {
+    if (!p || !seq || !st || !e) return fail(ADX_EINVAL, "adx_eval_structure: null argument");
+    double v = eval_structure(p->P, seq, st);
+    if (std::isnan(v)) return fail(ADX_EINVAL, "malformed structure '%s'", st);
+    *e = v;
+    return ADX_OK;
+}
+
+// ------------------------------------------------------------------ tables
+namespace {
+
+double boltz_d(double e_dcal) {
+    if (e_dcal >= INF_E / 2) return 0.0;
+    return std::exp(-e_dcal * 10.0 / kT_cal());
+}
+float boltz(double e_dcal) { return static_cast<float>(boltz_d(e_dcal)); }
+
+void build_tables(const EnergyParams &P, DevTables &T) {
+    std::memset(&T, 0, sizeof T);
+    for (int a = 1; a <= 7; a++) {
+        for (int b = 1; b <= 7; b++) T.stack[a][b] = boltz(P.stack[a][b]);
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++) {
+                T.mmH[a][x][y] = boltz(P.mmH[a][x][y]);
+                T.mmI[a][x][y] = boltz(P.mmI[a][x][y]);
+                T.mm1n[a][x][y] = boltz(P.mm1nI[a][x][y]);
+                T.mm23[a][x][y] = boltz(P.mm23I[a][x][y]);
+                T.mlstem[a][x][y] = boltz(ml_stem_energy(P, a, x, y));
+            }
+        for (int x = 0; x < 6; x++)
+            for (int y = 0; y < 6; y++)
+                T.ext[a][x][y] = boltz(ext_stem_energy(P, a, x == 5 ? -1 : x, y == 5 ? -1 : y));
+        T.termAU[a] = boltz(a > 2 ? P.TermAU : 0);
+        for (int b = 1; b <= 7; b++)
+            for (int x = 0; x < 5; x++)
+                for (int y = 0; y < 5; y++) {
+                    T.int11[a][b][x][y] = boltz(P.int11[a][b][x][y]);
+                    for (int z = 0; z < 5; z++) {
+                        T.int21[a][b][x][y][z] = boltz(P.int21[a][b][x][y][z]);
+                        for (int w = 0; w < 5; w++)
+                            T.int22[a][b][x][y][z][w] = boltz(P.int22[a][b][x][y][z][w]);
+                    }
+                }
+    }
+}
+
+struct Motif {
+    std::string seq, fold;
+    double energy_kcal = 0.0;
+    int mode = ADX_MOTIF_ADD;
+    bool present = false;
+};
+
+// Validate the ligand motif and compute its intrinsic energy (kcal/mol).
+adx_status prepare_motif(const EnergyParams &P, const Motif &m, double &eint, std::vector<int> &pt) {
+    const int L = static_cast<int>(m.seq.size());
+    if (L < 5 || L > MAX_MOTIF || static_cast<int>(m.fold.size()) != L)
+        return fail(ADX_EINVAL, "motif: sequence and fold must have equal length in [5, %d]", MAX_MOTIF);
+    if (m.fold.find('&') != std::string::npos)
+        return fail(ADX_EUNSUPPORTED, "motif: split (&) interior-loop motifs are not supported");
+    pt.assign(L, -1);
+    std::vector<int> stk;
+    for (int k = 0; k < L; k++) {
+        if (m.fold[k] == '(') stk.push_back(k);
+        else if (m.fold[k] == ')') {
+            if (stk.empty()) return fail(ADX_EINVAL, "motif: unbalanced fold '%s'", m.fold.c_str());
+            pt[stk.back()] = k;
+            pt[k] = stk.back();
+            stk.pop_back();
+        } else if (m.fold[k] != '.') {
+            return fail(ADX_EINVAL, "motif: bad character in fold '%s'", m.fold.c_str());
+        }
+    }
+    if (!stk.empty()) return fail(ADX_EINVAL, "motif: unbalanced fold '%s'", m.fold.c_str());
+    if (pt[0] != L - 1)
+        return fail(ADX_EUNSUPPORTED, "motif: the outermost pair must span the whole motif");
+    // every pair canonical, every hairpin >= TURN, every interior loop <= MAXLOOP
+    for (int k = 0; k < L; k++) {
+        if (pt[k] > k) {
+            if (!pair_type(base_code(m.seq[k]), base_code(m.seq[pt[k]])))
+                return fail(ADX_EINVAL, "motif: non-canonical pair (%d,%d)", k, pt[k]);
+            if (pt[k] - k - 1 < TURN) return fail(ADX_EINVAL, "motif: hairpin shorter than 3");
+            int nb = 0, p = -1, q = -1;
+            for (int t = k + 1; t < pt[k]; t++)
+                if (pt[t] > t) {
+                    if (++nb == 1) { p = t; q = pt[t]; }
+                    t = pt[t];
+                }
+            if (nb == 1 && (p - k - 1) + (pt[k] - q - 1) > MAXLOOP)
+                return fail(ADX_EUNSUPPORTED, "motif: interior loop larger than MAXLOOP");
+        }
+    }
+    eint = eval_structure(P, m.seq, m.fold);
+    if (std::isnan(eint)) return fail(ADX_EINVAL, "motif: cannot evaluate fold");
+    return ADX_OK;
+}
+
+void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double eint,
+                  const std::vector<int> &mpt, DevScaled &X) {
+    std::memset(&X, 0, sizeof X);
+    auto sp = [&](int k) { return std::pow(sigma, k); };
+    int n = 0;
+    for (int u = 0; u <= MAXLOOP; u++) {
+        for (int n1 = 0; n1 <= u; n1++) {
+            const int n2 = u - n1;
+            const int nl = std::max(n1, n2), ns = std::min(n1, n2);
+            TermDesc t;
+            t.n1 = static_cast<uint8_t>(n1);
+            t.n2 = static_cast<uint8_t>(n2);
+            t.u = static_cast<uint8_t>(u);
+            double f;
+            if (u == 0) {
+                t.kind = K_STACK;
+                f = 1.0;
+            } else if (ns == 0) {
+                t.kind = (nl == 1) ? K_BULGE1 : K_BULGE;
+                f = boltz_d(P.bulge[nl]);
+            } else if (ns == 1 && nl == 1) {
+                t.kind = K_I11;
+                f = 1.0;
+            } else if (ns == 1 && nl == 2) {
+                t.kind = (n1 == 1) ? K_I21 : K_I12;
+                f = 1.0;
+            } else if (ns == 1) {
+                t.kind = K_1N;
+                f = boltz_d(P.interior[nl + 1] + std::min(P.maxninio, (nl - ns) * P.ninio));
+            } else if (ns == 2 && nl == 2) {
+                t.kind = K_I22;
+                f = 1.0;
+            } else if (ns == 2 && nl == 3) {
+                t.kind = K_I23;
+                f = boltz_d(P.interior[5] + P.ninio);
+            } else {
+                t.kind = K_GENERIC;
+                f = boltz_d(P.interior[u] + std::min(P.maxninio, (nl - ns) * P.ninio));
+            }
+            t.f = static_cast<float>(f * sp(u + 2));
+            X.terms[n++] = t;
+        }
+        X.ncnt[u] = n;
+    }
+    X.ncnt[31] = n;
+    for (int k = 0; k < NMAX + 4; k++) X.sig[k] = static_cast<float>(sp(k));
+    for (int u = 0; u <= NMAX; u++) {
+        double e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + P.lxc * std::log(u / 30.0);
+        X.hp[u] = static_cast<float>(boltz_d(e) * sp(u + 2));
+    }
+    const double mlb = boltz_d(P.MLbase);
+    for (int t = 0; t <= NMAX; t++) X.pwml[t] = static_cast<float>(std::pow(mlb * sigma, t));
+    X.mlclosing = static_cast<float>(boltz_d(P.MLclosing) * sp(2));
+    X.mlbase_sig = static_cast<float>(mlb * sigma);
+    int ns = 0;
+    auto add_special = [&](const std::vector<std::pair<std::string, int>> &tab) {
+        for (auto &e : tab) {
+            if (ns >= MAX_SPECIAL_HP) break;
+            std::vector<uint8_t> codes(e.first.size());
+            for (size_t k = 0; k < e.first.size(); k++) codes[k] = static_cast<uint8_t>(base_code(e.first[k]));
+            X.sp_key[ns] = hp_key(codes.data(), 0, static_cast<int>(codes.size()));
+            X.sp_val[ns] = static_cast<float>(boltz_d(e.second) * sp(static_cast<int>(codes.size())));
+            ns++;
+        }
+    };
+    add_special(P.triloops);
+    add_special(P.tetraloops);
+    add_special(P.hexaloops);
+    X.n_special = ns;
+    X.log_sigma = std::log(sigma);
+    X.kT = kT_kcal();
+    if (m.present) {
+        const int L = static_cast<int>(m.seq.size());
+        X.motif_len = L;
+        for (int k = 0; k < L; k++) {
+            X.motif_code[k] = static_cast<uint8_t>(base_code(m.seq[k]));
+            X.motif_pt[k] = static_cast<int8_t>(mpt[k]);
+        }
+        const double beff = (m.mode == ADX_MOTIF_REPLACE) ? m.energy_kcal - eint : m.energy_kcal;
+        const double extra = boltz_d(eint * 100.0) * (boltz_d(beff * 100.0) - 1.0) * sp(L);
+        X.motif_extra = static_cast<float>(extra);
+    }
+}
+
+// Dot-bracket hard constraint (DB_DEFAULT | ENFORCE_BP, scoring.cc:61-62) ->
+// five byte arrays of length N+2: up, dn, ptn, enc, flg (see kernels.hip).
+adx_status build_constraint(const std::string &cst, int N, std::vector<uint8_t> &out) {
+    const int np = N + 2;
+    out.assign(5 * np, 0);
+    std::vector<int> partner(np, 0), enc(np, 0), unp(np, 1), flg(np, 0), stk;
+    for (int i = 1; i <= N; i++) {
+        const char c = cst.empty() ? '.' : cst[i - 1];
+        enc[i] = stk.empty() ? 0 : stk.back();
+        if (c == '(') stk.push_back(i);
+        else if (c == ')') {
+            if (stk.empty()) return fail(ADX_ECONSTRAINT, "unbalanced ')' in constraint '%s'", cst.c_str());
+            int a = stk.back();
+            stk.pop_back();
+            partner[a] = i;
+            partner[i] = a;
+            enc[i] = stk.empty() ? 0 : stk.back();
+        }
+    }
+    if (!stk.empty()) return fail(ADX_ECONSTRAINT, "unbalanced '(' in constraint '%s'", cst.c_str());
+    for (int i = 1; i <= N; i++) {
+        const char c = cst.empty() ? '.' : cst[i - 1];
+        if (c == 'x') flg[i] |= 1;
+        if (c == '<') flg[i] |= 2;
+        if (c == '>') flg[i] |= 4;
+        if (c == '|' || c == '<' || c == '>' || partner[i]) unp[i] = 0;
+    }
+    std::vector<int> up(np + 1, 0), dn(np, 0);
+    for (int i = N; i >= 1; i--) up[i] = unp[i] ? up[i + 1] + 1 : 0;
+    for (int i = 1; i <= N; i++) dn[i] = unp[i] ? dn[i - 1] + 1 : 0;
+    for (int k = 0; k < np; k++) {
+        out[k] = static_cast<uint8_t>(std::min(up[k], 255));
+        out[np + k] = static_cast<uint8_t>(std::min(dn[k], 255));
+        out[2 * np + k] = static_cast<uint8_t>(partner[k]);
+        out[3 * np + k] = static_cast<uint8_t>(enc[k]);
+        out[4 * np + k] = static_cast<uint8_t>(flg[k]);
+    }
+    return ADX_OK;
+}
+
+std::vector<uint8_t> encode(const std::string &s) {
+    std::vector<uint8_t> v(s.size());
+    for (size_t k = 0; k < s.size(); k++) v[k] = static_cast<uint8_t>(base_code(s[k]));
+    return v;
+}
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        reset();
+        n = count;
+        return hipMalloc(reinterpret_cast<void **>(&p), std::max<size_t>(count, 1) * sizeof(T));
+    }
+    hipError_t upload(const T *src, size_t count, hipStream_t s) {
+        hipError_t e = alloc(count);
+        if (e != hipSuccess) return e;
+        return hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+// One folding problem: energy tables, scaled constants, variants,
+// constraint blobs and score-term map on one device.
+struct Problem {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    const EnergyParams *P = nullptr;
+    int Nraw = 0, Nmax = 0;
+    Motif motif;
+    double motif_eint = 0.0;
+    std::vector<int> motif_pt;
+    double g0 = -0.30;  // assumed free energy per nucleotide for the pf scale
+    std::vector<DevVariant> variants;
+    std::vector<uint8_t> cons;
+    std::vector<uint8_t> ctx_seq;
+    std::vector<int> ctx_off;
+    std::vector<DevTermMap> tmap;
+    int n_terms = 0, n_ctx_eff = 1;
+    bool qbm = true;
+    DevBuf<DevTables> dT;
+    DevBuf<DevScaled> dX;
+    DevBuf<DevVariant> dV;
+    DevBuf<uint8_t> dCons, dCtxSeq;
+    DevBuf<int> dCtxOff;
+    DevBuf<DevTermMap> dTmap;
+    std::unique_ptr<DevTables> hT;
+    std::unique_ptr<DevScaled> hX;
+
+    ~Problem() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    double sigma() const { return std::exp(g0 / kT_kcal()); }
+
+    adx_status init_device() {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            return fail(ADX_ENODEV, "no HIP device visible (the engine requires a gfx950 GPU)");
+        if (device < 0 || device >= ndev) return fail(ADX_ENODEV, "device %d not present (%d visible)", device, ndev);
+        HIP_TRY(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(ADX_ENODEV, "device %d is %s, the kernels are built for gfx950", device, prop.gcnArchName);
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        return ADX_OK;
+    }
+
+    KArgs kargs() const {
+        KArgs ka;
+        ka.T = dT.p;
+        ka.X = dX.p;
+        ka.variants = dV.p;
+        ka.cons = dCons.p;
+        ka.ctx_seq = dCtxSeq.p;
+        ka.ctx_off = dCtxOff.p;
+        ka.tmap = dTmap.p;
+        ka.n_variants = static_cast<int>(variants.size());
+        ka.n_terms = n_terms;
+        ka.n_ctx_eff = n_ctx_eff;
+        ka.Nraw = Nraw;
+        ka.Nmax = Nmax;
+        ka.cells = Nmax >= 5 ? (Nmax - 4) * (Nmax - 3) / 2 : 1;
+        return ka;
+    }
+
+    adx_status choose_layout() {
+        KArgs ka = kargs();
+        const char *env = std::getenv("ADX_QBM");
+        const size_t with = lds_bytes(ka, true, NT), without = lds_bytes(ka, false, NT);
+        if (env) qbm = std::atoi(env) != 0;
+        else if (with * 2 <= LDS_MAX) qbm = true;
+        else if (without * 2 <= LDS_MAX) qbm = false;
+        else qbm = with <= LDS_MAX;
+        if (lds_bytes(ka, qbm, NT) > LDS_MAX)
+            return fail(ADX_EUNSUPPORTED, "sequence length %d needs %zu B of LDS (> %zu)", Nmax,
+                        lds_bytes(ka, qbm, NT), LDS_MAX);
+        return ADX_OK;
+    }
+
+    adx_status upload_scaled() {
+        build_scaled(*P, sigma(), motif, motif_eint, motif_pt, *hX);
+        HIP_TRY(dX.upload(hX.get(), 1, stream));
+        return ADX_OK;
+    }
+
+    adx_status upload_all() {
+        hT = std::make_unique<DevTables>();
+        hX = std::make_unique<DevScaled>();
+        build_tables(*P, *hT);
+        HIP_TRY(dT.upload(hT.get(), 1, stream));
+        adx_status s = upload_scaled();
+        if (s) return s;
+        HIP_TRY(dV.upload(variants.data(), variants.size(), stream));
+        HIP_TRY(dCons.upload(cons.data(), cons.size(), stream));
+        HIP_TRY(dCtxSeq.upload(ctx_seq.data(), ctx_seq.size(), stream));
+        HIP_TRY(dCtxOff.upload(ctx_off.data(), ctx_off.size(), stream));
+        HIP_TRY(dTmap.upload(tmap.data(), tmap.size(), stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return choose_layout();
+    }
+
+    // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
+    adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
+        HIP_TRY(launch_score(kargs(), qbm, dseqs, W, dscores, dterms, ddG, stream));
+        return ADX_OK;
+    }
+};
+
+// pick a pf scale from the ensemble energy of a reference sequence
+adx_status calibrate(Problem &pb, const std::vector<uint8_t> &codes) {
+    DevBuf<uint8_t> dseq;
+    DevBuf<double> dsc;
+    DevBuf<float> ddg;
+    HIP_TRY(dseq.upload(codes.data(), codes.size(), pb.stream));
+    HIP_TRY(dsc.alloc(1));
+    HIP_TRY(ddg.alloc(pb.variants.size()));
+    std::vector<float> g(pb.variants.size());
+    for (int attempt = 0; attempt < 6; attempt++) {
+        adx_status s = pb.upload_scaled();
+        if (s) return s;
+        s = pb.score(dseq.p, 1, dsc.p, nullptr, ddg.p);
+        if (s) return s;
+        HIP_TRY(hipMemcpyAsync(g.data(), ddg.p, g.size() * sizeof(float), hipMemcpyDeviceToHost, pb.stream));
+        HIP_TRY(hipStreamSynchronize(pb.stream));
+        // variant 0 is always the unconstrained apo ensemble of the first context
+        const double G = g[0];
+        const int N = pb.variants[0].N;
+        if (std::isfinite(G) && N > 0) {
+            const double g_new = std::min(-0.05, G / N);
+            if (std::fabs(g_new - pb.g0) < 1e-9) return ADX_OK;
+            pb.g0 = g_new;
+            return pb.upload_scaled();
+        }
+        pb.g0 *= 2.0;  // overflow: scale harder and retry
+    }
+    return fail(ADX_EINVAL, "could not find a partition-function scale for this sequence");
+}
+
+}  // namespace
+
+// ================================================================== fold layer
+struct adx_fold {
+    const adx_params *params = nullptr;
+    std::string seq;
+    int with_bppm = 0;
+    int device = 0;
+    std::string constraint;  // accumulated (last one wins, like a fresh DB constraint)
+    Motif motif;
+};
+
+extern "C" adx_status adx_fold_create(const adx_params *p, const char *seq, int with_bppm, int device,
+                                      adx_fold **out) {
+    if (!p || !seq || !out) return fail(ADX_EINVAL, "adx_fold_create: null argument");
+    const int N = static_cast<int>(std::strlen(seq));
+    if (N < 1 || N > NMAX) return fail(ADX_EINVAL, "sequence length %d outside [1, %d]", N, NMAX);
+    auto f = std::make_unique<adx_fold>();
+    f->params = p;
+    f->seq = seq;
+    for (auto &c : f->seq) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+    f->with_bppm = with_bppm;
+    f->device = device;
+    *out = f.release();
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_fold_add_motif(adx_fold *f, const char *mseq, const char *mfold, double e) {
+    if (!f || !mseq || !mfold) return fail(ADX_EINVAL, "adx_fold_add_motif: null argument");
+    f->motif.seq = mseq;
+    for (auto &c : f->motif.seq) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+    f->motif.fold = mfold;
+    f->motif.energy_kcal = e;
+    f->motif.present = true;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_fold_add_constraint(adx_fold *f, const char *db) {
+    if (!f || !db) return fail(ADX_EINVAL, "adx_fold_add_constraint: null argument");
+    if (std::strlen(db) != f->seq.size())
+        return fail(ADX_ECONSTRAINT, "constraint length %zu != sequence length %zu", std::strlen(db), f->seq.size());
+    std::vector<uint8_t> tmp;
+    adx_status s = build_constraint(db, static_cast<int>(f->seq.size()), tmp);
+    if (s) return s;
+    f->constraint = db;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_fold_pf(adx_fold *f, float *energy) {
+    if (!f || !energy) return fail(ADX_EINVAL, "adx_fold_pf: null argument");
+    Problem pb;
+    pb.device = f->device;
+    pb.P = &f->params->P;
+    adx_status s = pb.init_device();
+    if (s) return s;
+    const int N = static_cast<int>(f->seq.size());
+    pb.Nraw = pb.Nmax = N;
+    pb.motif = f->motif;
+    if (pb.motif.present) {
+        s = prepare_motif(*pb.P, pb.motif, pb.motif_eint, pb.motif_pt);
+        if (s) return s;
+    }
+    // variant 0: the ensemble this fold compound currently describes
+    std::vector<uint8_t> c;
+    s = build_constraint(f->constraint, N, c);
+    if (s) return s;
+    pb.cons = c;
+    pb.variants.push_back(DevVariant{N, 0, -1, 0, pb.motif.present ? 1 : 0, 0});
+    pb.ctx_seq.assign(1, 0);
+    pb.ctx_off.assign(4, 0);
+    pb.tmap.assign(1, DevTermMap{0, 0, 1, 0.0});
+    pb.n_terms = 0;
+    s = pb.upload_all();
+    if (s) return s;
+    std::vector<uint8_t> codes = encode(f->seq);
+    DevBuf<uint8_t> dseq;
+    DevBuf<double> dsc;
+    DevBuf<float> ddg;
+    HIP_TRY(dseq.upload(codes.data(), codes.size(), pb.stream));
+    HIP_TRY(dsc.alloc(1));
+    HIP_TRY(ddg.alloc(1));
+    float g = NAN;
+    for (int attempt = 0; attempt < 6; attempt++) {
+        s = pb.score(dseq.p, 1, dsc.p, nullptr, ddg.p);
+        if (s) return s;
+        HIP_TRY(hipMemcpyAsync(&g, ddg.p, sizeof(float), hipMemcpyDeviceToHost, pb.stream));
+        HIP_TRY(hipStreamSynchronize(pb.stream));
+        if (std::isfinite(g) || std::isinf(g) && g > 0) {
+            // +inf = empty (constrained) ensemble; recalibrate once for accuracy
+            if (attempt == 0 && std::isfinite(g) && N > 0) {
+                pb.g0 = std::min(-0.05, static_cast<double>(g) / N);
+                s = pb.upload_scaled();
+                if (s) return s;
+                continue;
+            }
+            break;
+        }
+        pb.g0 *= 2.0;
+        s = pb.upload_scaled();
+        if (s) return s;
+    }
+    *energy = g;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_fold_bpp(adx_fold *f, int i, int j, double *prob) {
+    (void)i;
+    (void)j;
+    (void)prob;
+    if (!f) return fail(ADX_EINVAL, "adx_fold_bpp: null argument");
+    return fail(ADX_EUNSUPPORTED, "base-pair probabilities (outside pass) are not built yet");
+}
+
+extern "C" void adx_fold_free(adx_fold *f) { delete f; }
+
+// ================================================================== MC layer
+struct adx_ctx {
+    Problem pb;
+    std::string templ;
+    std::vector<std::string> macrostates;
+    std::vector<adx_term> terms;
+    adx_thermostat thermo{};
+    int n_contexts = 0;
+    std::vector<int> mut;
+    std::vector<int> clo_off, clo_pos, clo_err;
+    std::vector<uint8_t> clo_par;
+    std::vector<std::string> clo_msg;
+    // walker state
+    int W = 0;
+    long long step = 0;
+    DevBuf<uint8_t> cur_seq;
+    DevBuf<double> cur_score, last_diff, auto_T, train;
+    DevBuf<uint32_t> mtA, mtC;
+    DevBuf<int64_t> counters;
+    DevBuf<int> ntrain, err;
+    DevBuf<int> d_mut, d_clo_off, d_clo_pos, d_clo_err;
+    DevBuf<uint8_t> d_clo_par;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0.0;
+
+    ~adx_ctx() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    }
+};
+
+namespace {
+
+const char *move_error_text(int code) {
+    switch (code) {
+    case 1: return "mismatched base-pair in macrostate";
+    case 2: return "position can be mutated, but it's base-paired to a position which can't be";
+    case 3: return "no way to satisfy all base pairing constraints.";
+    default: return "unknown move error";
+    }
+}
+
+// mutate_recursively (sampling.cc:195-282) on the template, recording the
+// closure of `pos` with its base parity and the first error the reference
+// would throw.  The result does not depend on the base chosen.
+int closure(const std::string &seq, const std::vector<std::string> &ms, int pos,
+            std::vector<std::pair<int, int>> &out) {
+    const int n = static_cast<int>(seq.size());
+    std::vector<int> par(n, -1);
+    // recursive DFS in the reference's order
+    std::function<int(int, int)> rec = [&](int p, int parity) -> int {
+        par[p] = parity;
+        out.push_back({p, parity});
+        for (const auto &mac : ms) {
+            char open, close;
+            int stepv;
+            if (mac[p] == '(') { open = '('; close = ')'; stepv = 1; }
+            else if (mac[p] == ')') { open = ')'; close = '('; stepv = -1; }
+            else continue;
+            int level = 1, partner = p;
+            while (level != 0) {
+                partner += stepv;
+                if (partner < 0 || partner >= n) return 1;
+                level += (mac[partner] == open);
+                level -= (mac[partner] == close);
+            }
+            if (!std::isupper(static_cast<unsigned char>(seq[partner]))) return 2;
+            if (par[partner] < 0) {
+                int rc = rec(partner, parity ^ 1);
+                if (rc) return rc;
+            } else if (par[partner] != (parity ^ 1)) {
+                return 3;
+            }
+        }
+        return 0;
+    };
+    return rec(pos, 0);
+}
+
+}  // namespace
+
+extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
+    if (!d || !out || !d->params || !d->sequence) return fail(ADX_EINVAL, "adx_ctx_create: null argument");
+    auto c = std::make_unique<adx_ctx>();
+    Problem &pb = c->pb;
+    pb.device = d->device;
+    pb.P = &d->params->P;
+    c->templ = d->sequence;
+    const int N = static_cast<int>(c->templ.size());
+    if (N < 1) return fail(ADX_EINVAL, "empty sequence");
+    for (int m = 0; m < d->n_macrostates; m++) {
+        std::string s = d->macrostates[m];
+        if (static_cast<int>(s.size()) != N)
+            return fail(ADX_EINVAL, "constraint length doesn't match sequence length");
+        c->macrostates.push_back(s);
+    }
+    if (d->n_terms < 0 || d->n_terms > MAX_TERMS) return fail(ADX_EINVAL, "n_terms out of range");
+    for (int t = 0; t < d->n_terms; t++) {
+        const adx_term &T = d->terms[t];
+        if (T.macrostate < 0 || T.macrostate >= d->n_macrostates)
+            return fail(ADX_EINVAL, "term %d names macrostate %d (have %d)", t, T.macrostate, d->n_macrostates);
+        if (T.condition != ADX_APO && T.condition != ADX_HOLO) return fail(ADX_EINVAL, "bad condition");
+        c->terms.push_back(T);
+    }
+    c->thermo = d->thermostat;
+    if (c->thermo.kind == ADX_THERMO_ANNEAL && c->thermo.cycle_len <= 0)
+        return fail(ADX_EINVAL, "annealing cycle length must be positive");
+    if (c->thermo.kind == ADX_THERMO_AUTO && c->thermo.period <= 0)
+        return fail(ADX_EINVAL, "auto thermostat training period must be positive");
+    if (c->thermo.kind < 0 || c->thermo.kind > 2) return fail(ADX_EINVAL, "bad thermostat kind");
+
+    adx_status s = pb.init_device();
+    if (s) return s;
+    pb.Nraw = N;
+    // motif
+    if (d->aptamer_seq && d->aptamer_fold) {
+        pb.motif.seq = d->aptamer_seq;
+        for (auto &ch : pb.motif.seq) ch = static_cast<char>(std::toupper(static_cast<unsigned char>(ch)));
+        pb.motif.fold = d->aptamer_fold;
+        pb.motif.energy_kcal = d->aptamer_energy_kcal;
+        pb.motif.mode = d->motif_mode;
+        pb.motif.present = true;
+        s = prepare_motif(*pb.P, pb.motif, pb.motif_eint, pb.motif_pt);
+        if (s) return s;
+    }
+    // contexts (ScoreFunction::evaluate scoring.cc:123-132, map order)
+    c->n_contexts = d->n_contexts;
+    pb.n_ctx_eff = std::max(1, d->n_contexts);
+    pb.n_terms = static_cast<int>(c->terms.size());
+    pb.ctx_seq.clear();
+    pb.ctx_off.clear();
+    std::vector<int> ctxN;
+    for (int k = 0; k < pb.n_ctx_eff; k++) {
+        std::string b, a;
+        if (d->n_contexts > 0) {
+            b = d->contexts[k].before ? d->contexts[k].before : "";
+            a = d->contexts[k].after ? d->contexts[k].after : "";
+        }
+        pb.ctx_off.push_back(static_cast<int>(pb.ctx_seq.size()));
+        pb.ctx_off.push_back(static_cast<int>(b.size()));
+        for (char ch : b) pb.ctx_seq.push_back(static_cast<uint8_t>(base_code(ch)));
+        pb.ctx_off.push_back(static_cast<int>(pb.ctx_seq.size()));
+        pb.ctx_off.push_back(static_cast<int>(a.size()));
+        for (char ch : a) pb.ctx_seq.push_back(static_cast<uint8_t>(base_code(ch)));
+        ctxN.push_back(static_cast<int>(b.size() + a.size()) + N);
+    }
+    if (pb.ctx_seq.empty()) pb.ctx_seq.push_back(0);
+    pb.Nmax = *std::max_element(ctxN.begin(), ctxN.end());
+    if (pb.Nmax > NMAX) return fail(ADX_EUNSUPPORTED, "folded length %d exceeds %d", pb.Nmax, NMAX);
+    // variants: per context, (condition, macrostate | free); holo == apo without an aptamer
+    std::map<std::tuple<int, int, int>, int> vindex;
+    auto variant = [&](int ctx, int cond, int mac) -> int {
+        if (!pb.motif.present) cond = ADX_APO;
+        auto key = std::make_tuple(ctx, cond, mac);
+        auto it = vindex.find(key);
+        if (it != vindex.end()) return it->second;
+        const int Nc = ctxN[ctx];
+        std::string cst;
+        if (mac >= 0) {
+            const int lb = pb.ctx_off[4 * ctx + 1];
+            cst = std::string(lb, '.') + c->macrostates[mac] + std::string(Nc - lb - N, '.');
+        }
+        std::vector<uint8_t> blob;
+        adx_status st = build_constraint(cst, Nc, blob);
+        if (st) return -1;
+        DevVariant v{Nc, pb.ctx_off[4 * ctx + 1], d->n_contexts > 0 ? ctx : -1,
+                     static_cast<int>(pb.cons.size()), cond == ADX_HOLO ? 1 : 0, 0};
+        pb.cons.insert(pb.cons.end(), blob.begin(), blob.end());
+        const int id = static_cast<int>(pb.variants.size());
+        pb.variants.push_back(v);
+        vindex[key] = id;
+        return id;
+    };
+    variant(0, ADX_APO, -1);  // variant 0 = apo ensemble (calibration anchor)
+    for (int k = 0; k < pb.n_ctx_eff; k++) {
+        for (auto &T : c->terms) {
+            const int vf = variant(k, T.condition, -1);
+            const int vc = variant(k, T.condition, T.macrostate);
+            if (vf < 0 || vc < 0) return ADX_ECONSTRAINT;
+            pb.tmap.push_back(DevTermMap{vf, vc, T.favorable, T.weight});
+        }
+    }
+    if (pb.tmap.empty()) pb.tmap.push_back(DevTermMap{0, 0, 1, 0.0});
+    if (static_cast<int>(pb.variants.size()) > MAX_VARIANTS) return fail(ADX_EUNSUPPORTED, "too many fold variants");
+    // moves: freely mutable positions and their closures
+    for (int i = 0; i < N; i++) {
+        bool free_ = std::isupper(static_cast<unsigned char>(c->templ[i])) != 0;
+        for (auto &m : c->macrostates)
+            if (m[i] == ')') free_ = false;
+        if (free_) c->mut.push_back(i);
+    }
+    c->clo_off.push_back(0);
+    for (int pos : c->mut) {
+        std::vector<std::pair<int, int>> cl;
+        const int rc = closure(c->templ, c->macrostates, pos, cl);
+        c->clo_err.push_back(rc);
+        if (rc == 0)
+            for (auto &pp : cl) {
+                c->clo_pos.push_back(pp.first);
+                c->clo_par.push_back(static_cast<uint8_t>(pp.second));
+            }
+        c->clo_off.push_back(static_cast<int>(c->clo_pos.size()));
+    }
+    if (c->clo_pos.empty()) { c->clo_pos.push_back(0); c->clo_par.push_back(0); }
+    s = pb.upload_all();
+    if (s) return s;
+    s = calibrate(pb, encode(c->templ));
+    if (s) return s;
+    HIP_TRY(hipEventCreate(&c->ev0));
+    HIP_TRY(hipEventCreate(&c->ev1));
+    HIP_TRY(c->d_mut.upload(c->mut.data(), c->mut.size(), pb.stream));
+    HIP_TRY(c->d_clo_off.upload(c->clo_off.data(), c->clo_off.size(), pb.stream));
+    HIP_TRY(c->d_clo_pos.upload(c->clo_pos.data(), c->clo_pos.size(), pb.stream));
+    HIP_TRY(c->d_clo_par.upload(c->clo_par.data(), c->clo_par.size(), pb.stream));
+    HIP_TRY(c->d_clo_err.upload(c->clo_err.data(), c->clo_err.size(), pb.stream));
+    HIP_TRY(hipStreamSynchronize(pb.stream));
+    *out = c.release();
+    return ADX_OK;
+}
+
+extern "C" void adx_ctx_destroy(adx_ctx *c) { delete c; }
+
+extern "C" adx_status adx_ctx_info(const adx_ctx *c, adx_info *info) {
+    if (!c || !info) return fail(ADX_EINVAL, "adx_ctx_info: null argument");
+    info->length = c->pb.Nraw;
+    info->n_variants = static_cast<int>(c->pb.variants.size());
+    info->n_terms = c->pb.n_terms;
+    info->n_mutable = static_cast<int>(c->mut.size());
+    info->max_walkers = 1 << 24;
+    info->scale_per_nt = c->pb.sigma();
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_variant_desc(const adx_ctx *c, int v, int *ctx, int *cond, int *mac) {
+    if (!c || v < 0 || v >= static_cast<int>(c->pb.variants.size())) return fail(ADX_EINVAL, "bad variant");
+    const DevVariant &V = c->pb.variants[v];
+    if (ctx) *ctx = V.ctx;
+    if (cond) *cond = V.motif ? ADX_HOLO : ADX_APO;
+    if (mac) {
+        *mac = -1;
+        for (size_t t = 0; t < c->pb.tmap.size(); t++)
+            if (c->pb.tmap[t].vcons == v && c->pb.n_terms > 0)
+                *mac = c->terms[t % c->pb.n_terms].macrostate;
+    }
+    return ADX_OK;
+}
+
+static void mt_seed_host(uint32_t seed, uint32_t *mt) {
+    mt[0] = seed;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + static_cast<uint32_t>(i);
+    mt[624] = 624;
+}
+
+extern "C" adx_status adx_walkers_init(adx_ctx *c, int W, const char *seqs, const uint32_t *seeds) {
+    if (!c || W <= 0 || !seeds) return fail(ADX_EINVAL, "adx_walkers_init: bad argument");
+    Problem &pb = c->pb;
+    const int N = pb.Nraw;
+    if (c->mut.empty()) return fail(ADX_EMOVE, "no freely mutable positions (vector index out of range)");
+    std::vector<uint8_t> codes(size_t(W) * N);
+    for (int w = 0; w < W; w++)
+        for (int k = 0; k < N; k++) {
+            const char ch = seqs ? seqs[size_t(w) * N + k] : c->templ[k];
+            codes[size_t(w) * N + k] = static_cast<uint8_t>(base_code(ch));
+        }
+    std::vector<uint32_t> mt(size_t(W) * MT_WORDS);
+    for (int w = 0; w < W; w++) mt_seed_host(seeds[w], &mt[size_t(w) * MT_WORDS]);
+    c->W = W;
+    c->step = 0;
+    HIP_TRY(c->cur_seq.upload(codes.data(), codes.size(), pb.stream));
+    HIP_TRY(c->mtA.upload(mt.data(), mt.size(), pb.stream));
+    HIP_TRY(c->mtC.upload(mt.data(), mt.size(), pb.stream));
+    HIP_TRY(c->cur_score.alloc(W));
+    HIP_TRY(c->last_diff.alloc(W));
+    HIP_TRY(c->auto_T.alloc(W));
+    HIP_TRY(c->counters.alloc(size_t(W) * 4));
+    HIP_TRY(c->ntrain.alloc(W));
+    HIP_TRY(c->err.alloc(W));
+    const int period = std::max(1, c->thermo.period);
+    HIP_TRY(c->train.alloc(c->thermo.kind == ADX_THERMO_AUTO ? size_t(W) * period : 1));
+    HIP_TRY(hipMemsetAsync(c->last_diff.p, 0, sizeof(double) * W, pb.stream));
+    HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(int64_t) * W * 4, pb.stream));
+    HIP_TRY(hipMemsetAsync(c->ntrain.p, 0, sizeof(int) * W, pb.stream));
+    HIP_TRY(hipMemsetAsync(c->err.p, 0, sizeof(int) * W, pb.stream));
+    std::vector<double> t0(W, c->thermo.t_init);
+    HIP_TRY(hipMemcpyAsync(c->auto_T.p, t0.data(), sizeof(double) * W, hipMemcpyHostToDevice, pb.stream));
+    // initial score (sampling.cc:40)
+    adx_status s = pb.score(c->cur_seq.p, W, c->cur_score.p, nullptr, nullptr);
+    if (s) return s;
+    HIP_TRY(hipStreamSynchronize(pb.stream));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
+    if (!c) return fail(ADX_EINVAL, "adx_run_steps: null context");
+    if (c->W <= 0) return fail(ADX_ESTATE, "adx_run_steps before adx_walkers_init");
+    if (steps <= 0) return ADX_OK;
+    Problem &pb = c->pb;
+    StepArgs st{};
+    st.cur_seq = c->cur_seq.p;
+    st.cur_score = c->cur_score.p;
+    st.mtA = c->mtA.p;
+    st.mtC = c->mtC.p;
+    st.counters = c->counters.p;
+    st.last_diff = c->last_diff.p;
+    st.auto_T = c->auto_T.p;
+    st.train = c->train.p;
+    st.ntrain = c->ntrain.p;
+    st.err = c->err.p;
+    st.mut = c->d_mut.p;
+    st.clo_off = c->d_clo_off.p;
+    st.clo_pos = c->d_clo_pos.p;
+    st.clo_par = c->d_clo_par.p;
+    st.clo_err = c->d_clo_err.p;
+    st.M = static_cast<int>(c->mut.size());
+    st.thermo_kind = c->thermo.kind;
+    st.t_fixed = c->thermo.t_fixed;
+    st.t_hi = c->thermo.t_hi;
+    st.t_lo = c->thermo.t_lo;
+    st.cycle_len = std::max(1, c->thermo.cycle_len);
+    st.target_rate = c->thermo.target_rate;
+    st.period = std::max(1, c->thermo.period);
+    st.step0 = c->step;
+    st.nsteps = steps;
+    st.W = c->W;
+    const int W = c->W;
+    const int ntt = pb.n_terms * pb.n_ctx_eff;
+    DevBuf<int32_t> tpos, tout;
+    DevBuf<int8_t> tbase;
+    DevBuf<double> ttemp, tprop, tcur, tu, tterms;
+    const size_t R = size_t(steps) * W;
+    if (trace) {
+        HIP_TRY(tpos.alloc(R));
+        HIP_TRY(tout.alloc(R));
+        HIP_TRY(tbase.alloc(R));
+        HIP_TRY(ttemp.alloc(R));
+        HIP_TRY(tprop.alloc(R));
+        HIP_TRY(tcur.alloc(R));
+        HIP_TRY(tu.alloc(R));
+        HIP_TRY(tterms.alloc(R * std::max(1, ntt)));
+        st.tr_pos = tpos.p;
+        st.tr_outcome = tout.p;
+        st.tr_base = tbase.p;
+        st.tr_temp = ttemp.p;
+        st.tr_prop = tprop.p;
+        st.tr_cur = tcur.p;
+        st.tr_u = tu.p;
+        st.tr_terms = ntt > 0 ? tterms.p : nullptr;
+    }
+    HIP_TRY(hipEventRecord(c->ev0, pb.stream));
+    HIP_TRY(launch_steps(pb.kargs(), pb.qbm, st, pb.stream));
+    HIP_TRY(hipEventRecord(c->ev1, pb.stream));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last_ms = ms;
+    c->step += steps;
+    std::vector<int> errs(W);
+    HIP_TRY(hipMemcpy(errs.data(), c->err.p, sizeof(int) * W, hipMemcpyDeviceToHost));
+    if (trace) {
+        std::vector<int8_t> b(R);
+        if (trace->position) HIP_TRY(hipMemcpy(trace->position, tpos.p, R * 4, hipMemcpyDeviceToHost));
+        if (trace->outcome) HIP_TRY(hipMemcpy(trace->outcome, tout.p, R * 4, hipMemcpyDeviceToHost));
+        if (trace->base) {
+            HIP_TRY(hipMemcpy(b.data(), tbase.p, R, hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < R; k++) trace->base[k] = b[k] >= 1 && b[k] <= 4 ? "ACGU"[b[k] - 1] : 'N';
+        }
+        if (trace->temperature) HIP_TRY(hipMemcpy(trace->temperature, ttemp.p, R * 8, hipMemcpyDeviceToHost));
+        if (trace->proposed_score) HIP_TRY(hipMemcpy(trace->proposed_score, tprop.p, R * 8, hipMemcpyDeviceToHost));
+        if (trace->current_score) HIP_TRY(hipMemcpy(trace->current_score, tcur.p, R * 8, hipMemcpyDeviceToHost));
+        if (trace->random_threshold) HIP_TRY(hipMemcpy(trace->random_threshold, tu.p, R * 8, hipMemcpyDeviceToHost));
+        if (trace->term_values && ntt > 0)
+            HIP_TRY(hipMemcpy(trace->term_values, tterms.p, R * ntt * 8, hipMemcpyDeviceToHost));
+    }
+    for (int w = 0; w < W; w++)
+        if (errs[w]) return fail(ADX_EMOVE, "walker %d: %s", w, move_error_text(errs[w]));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_last_kernel_ms(const adx_ctx *c, double *ms) {
+    if (!c || !ms) return fail(ADX_EINVAL, "adx_last_kernel_ms: null argument");
+    *ms = c->last_ms;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_walkers_download(adx_ctx *c, char *seqs, double *scores, int64_t *counters) {
+    if (!c) return fail(ADX_EINVAL, "adx_walkers_download: null context");
+    if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
+    const int W = c->W, N = c->pb.Nraw;
+    HIP_TRY(hipStreamSynchronize(c->pb.stream));
+    if (seqs) {
+        std::vector<uint8_t> codes(size_t(W) * N);
+        HIP_TRY(hipMemcpy(codes.data(), c->cur_seq.p, codes.size(), hipMemcpyDeviceToHost));
+        for (int w = 0; w < W; w++)
+            for (int k = 0; k < N; k++) {
+                const uint8_t b = codes[size_t(w) * N + k];
+                char ch = b >= 1 && b <= 4 ? "ACGU"[b - 1] : 'N';
+                if (std::islower(static_cast<unsigned char>(c->templ[k])))
+                    ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+                seqs[size_t(w) * N + k] = ch;
+            }
+    }
+    if (scores) HIP_TRY(hipMemcpy(scores, c->cur_score.p, sizeof(double) * W, hipMemcpyDeviceToHost));
+    if (counters) HIP_TRY(hipMemcpy(counters, c->counters.p, sizeof(int64_t) * W * 4, hipMemcpyDeviceToHost));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_score_batch(adx_ctx *c, int W, const char *seqs, double *scores,
+                                      double *term_values, float *dG) {
+    if (!c || W <= 0 || !seqs || !scores) return fail(ADX_EINVAL, "adx_score_batch: bad argument");
+    Problem &pb = c->pb;
+    const int N = pb.Nraw;
+    std::vector<uint8_t> codes(size_t(W) * N);
+    for (size_t k = 0; k < codes.size(); k++) codes[k] = static_cast<uint8_t>(base_code(seqs[k]));
+    const int V = static_cast<int>(pb.variants.size());
+    const int ntt = pb.n_terms * pb.n_ctx_eff;
+    DevBuf<uint8_t> dseq;
+    DevBuf<double> dsc, dterms;
+    DevBuf<float> ddg;
+    HIP_TRY(dseq.upload(codes.data(), codes.size(), pb.stream));
+    HIP_TRY(dsc.alloc(W));
+    HIP_TRY(dterms.alloc(size_t(W) * std::max(1, ntt)));
+    HIP_TRY(ddg.alloc(size_t(W) * V));
+    HIP_TRY(hipEventRecord(c->ev0, pb.stream));
+    adx_status s = pb.score(dseq.p, W, dsc.p, ntt > 0 ? dterms.p : nullptr, ddg.p);
+    if (s) return s;
+    HIP_TRY(hipEventRecord(c->ev1, pb.stream));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last_ms = ms;
+    HIP_TRY(hipMemcpy(scores, dsc.p, sizeof(double) * W, hipMemcpyDeviceToHost));
+    if (term_values && ntt > 0)
+        HIP_TRY(hipMemcpy(term_values, dterms.p, sizeof(double) * W * ntt, hipMemcpyDeviceToHost));
+    if (dG) HIP_TRY(hipMemcpy(dG, ddg.p, sizeof(float) * W * V, hipMemcpyDeviceToHost));
+    return ADX_OK;
+}

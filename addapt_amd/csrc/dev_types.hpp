@@ -1,0 +1,148 @@
+// Structures shared by the host setup code and the gfx950 kernels.
+//
+// HBM layout (all read-only during a launch unless noted):
+//   DevTables  -- FP32 Boltzmann factors of the energy model (~230 KB, L2
+//                 resident; loaded per term by the fold kernels)
+//   DevScaled  -- per-context quantities that fold in the pf scale sigma^k
+//                 (interior-loop term list, hairpin/ML power tables, ...)
+//   constraint blobs -- per (context, macrostate) 5 byte arrays of N+2
+//   walker state (read/write): sequences W*N (codes 1..4), scores W (f64),
+//                 mt19937 streams A and C (W * 2 * 625 u32), counters W*4.
+#pragma once
+
+#include <cstdint>
+
+namespace adx {
+
+constexpr int NMAX = 255;          // positions (u8 indices in LDS lists)
+constexpr int MAX_VARIANTS = 64;
+constexpr int MAX_TERMS = 64;
+constexpr int MAX_SPECIAL_HP = 96;
+constexpr int MAX_MOTIF = 96;
+constexpr int N_INT_TERMS = 496;   // (n1, n2) with n1 + n2 <= 30
+constexpr int MT_WORDS = 625;      // 624 state words + index
+
+enum TermKind : uint8_t {
+    K_GENERIC = 0,
+    K_STACK = 1,
+    K_BULGE1 = 2,
+    K_BULGE = 3,
+    K_I11 = 4,
+    K_I21 = 5,   // n1 = 1, n2 = 2
+    K_I12 = 6,   // n1 = 2, n2 = 1
+    K_I22 = 7,
+    K_I23 = 8,   // 2x3 and 3x2
+    K_1N = 9,    // 1xn and nx1, n >= 3
+};
+
+struct TermDesc {          // one interior-loop shape, sorted by u = n1 + n2
+    uint8_t n1, n2, kind, u;
+    float f;               // shape-only Boltzmann factor * sigma^(u+2)
+};
+
+struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
+    float stack[8][8];
+    float mmH[8][5][5];
+    float mmI[8][5][5];
+    float mm1n[8][5][5];
+    float mm23[8][5][5];
+    float mlstem[8][5][5];   // mismatchM * TermAU * MLintern (dangles = 2)
+    float ext[8][6][6];      // exterior stem; neighbour code 5 = absent
+    float termAU[8];
+    float int11[8][8][5][5];
+    float int21[8][8][5][5][5];
+    float int22[8][8][5][5][5][5];
+};
+
+struct DevScaled {
+    TermDesc terms[N_INT_TERMS];
+    int ncnt[32];            // number of terms with u <= k
+    float sig[NMAX + 4];     // sigma^k
+    float hp[NMAX + 1];      // hairpin length factor * sigma^(u+2)
+    float pwml[NMAX + 1];    // (expMLbase * sigma)^t
+    float mlclosing;         // expMLclosing * sigma^2
+    float mlbase_sig;        // expMLbase * sigma
+    int n_special;
+    uint32_t sp_key[MAX_SPECIAL_HP];
+    float sp_val[MAX_SPECIAL_HP];   // exp(-E_special) * sigma^(u+2)
+    double log_sigma;
+    double kT;               // kcal/mol
+    // ligand motif (vrna_sc_add_hi_motif)
+    int motif_len;
+    uint8_t motif_code[MAX_MOTIF];
+    int8_t motif_pt[MAX_MOTIF];     // partner offset or -1
+    float motif_extra;              // exp(-Eint)(exp(-bonus)-1) * sigma^L
+};
+
+struct DevVariant {
+    int N;            // folded length (context-padded)
+    int before_len;   // context prefix length
+    int ctx;          // context index (-1 none)
+    int cons_off;     // byte offset of this variant's constraint arrays
+    int motif;        // 1 = holo (ligand motif active)
+    int pad;
+};
+
+struct DevTermMap {   // per (context, term)
+    int vfree, vcons;
+    int favorable;
+    double weight;
+};
+
+// Special-hairpin key: 3 bits per base of the closing-pair-inclusive loop.
+__host__ __device__ inline uint32_t hp_key(const uint8_t *S, int i, int len) {
+    uint32_t k = static_cast<uint32_t>(len);
+    for (int t = 0; t < len; t++) k = (k << 3) | S[i + t];
+    return k;
+}
+
+struct KArgs {
+    const DevTables *T;
+    const DevScaled *X;
+    const DevVariant *variants;
+    const uint8_t *cons;        // constraint blobs
+    const uint8_t *ctx_seq;     // concatenated before/after context codes
+    const int *ctx_off;         // per context: before offset, before len, after offset, after len
+    const DevTermMap *tmap;     // [n_ctx_eff * n_terms]
+    int n_variants;
+    int n_terms;
+    int n_ctx_eff;              // max(1, contexts)
+    int Nraw;                   // raw device length
+    int Nmax;                   // max folded length over variants
+    int cells;                  // (Nmax-4)(Nmax-3)/2
+};
+
+// Monte Carlo state (device, read/write).
+struct StepArgs {
+    uint8_t *cur_seq;           // W * Nraw codes
+    double *cur_score;          // W
+    uint32_t *mtA, *mtC;        // W * MT_WORDS
+    int64_t *counters;          // W * 4
+    double *last_diff;          // W (score_diff carried across steps)
+    double *auto_T;             // W
+    double *train;              // W * period
+    int *ntrain;                // W
+    int *err;                   // W (0 ok, else move error code)
+    const int *mut;             // freely mutable positions (0-based raw), M
+    const int *clo_off;         // M + 1
+    const int *clo_pos;         // closure positions (0-based raw)
+    const uint8_t *clo_par;     // 0 same base, 1 complement
+    const int *clo_err;         // M
+    int M;
+    int thermo_kind;
+    double t_fixed, t_hi, t_lo;
+    int cycle_len;
+    double target_rate;
+    int period;
+    long long step0;            // global step index of the first step of this launch
+    int nsteps;
+    int W;
+    // optional trace (nullptr when off), step-major [s * W + w]
+    int32_t *tr_pos;
+    int8_t *tr_base;
+    int32_t *tr_outcome;
+    double *tr_temp, *tr_prop, *tr_cur, *tr_u;
+    double *tr_terms;           // [(s*W + w) * n_terms_total]
+};
+
+}  // namespace adx

@@ -1,0 +1,192 @@
+/*
+ * addapt_gpu.h -- C ABI of the MI355X (gfx950) fold -> score -> accept engine.
+ *
+ * Plain C, plain pointers and sizes, status codes, no exceptions, no torch
+ * types.  Library: addapt_amd/_lib/libaddapt_gpu.so (built by
+ * __graft_entry__.build()).  All calls are synchronous; one context per GPU
+ * per host thread; calls on one context must be serialised by the caller.
+ *
+ * Two layers, both replacing the reference's FFI into ViennaRNA
+ * (/root/reference/src/scoring.cc:6-11 includes, 37-103 call sites):
+ *
+ *  (1) the per-fold layer adx_fold_* -- one entry point per ViennaRNA symbol
+ *      the reference binds, for code that keeps addapt's RnaFold interface
+ *      (scoring.hh:42-55, ViennaRnaFold scoring.cc:17-103);
+ *
+ *  (2) the batched Monte Carlo layer adx_ctx_* / adx_walkers_* / adx_run_steps
+ *      / adx_score_batch -- thousands of independent walkers, each step of
+ *      MonteCarlo::apply (sampling.cc:55-99) fused into one HIP kernel.
+ */
+#ifndef ADDAPT_GPU_H
+#define ADDAPT_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADX_ABI_VERSION 1
+
+typedef enum adx_status {
+    ADX_OK = 0,
+    ADX_EINVAL = 1,      /* bad argument / malformed input */
+    ADX_EHIP = 2,        /* HIP runtime error */
+    ADX_ECONSTRAINT = 3, /* malformed dot-bracket constraint */
+    ADX_EPARAM = 4,      /* energy-parameter file could not be read */
+    ADX_ENOMEM = 5,      /* allocation failed */
+    ADX_EMOVE = 6,       /* mutation move failed (sampling.cc:256,265,279) */
+    ADX_ESTATE = 7,      /* call out of order (e.g. run before walkers_init) */
+    ADX_ENODEV = 8,      /* no gfx950 device visible */
+    ADX_EUNSUPPORTED = 9 /* feature not available on the GPU path */
+} adx_status;
+
+/* Thread-local message for the last non-OK status. */
+const char *adx_last_error(void);
+int adx_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * Energy parameters (ViennaRNA 2.0 parameter-file layout).  Replaces the
+ * implicit vrna_md_set_default() model (scoring.cc:80-83): 37 C, dangles=2,
+ * special hairpins, TURN=3, MAXLOOP=30.
+ * ---------------------------------------------------------------------- */
+typedef struct adx_params adx_params;
+adx_status adx_params_load(const char *par_path, adx_params **out);
+void adx_params_free(adx_params *p);
+/* kT at 37 C in kcal/mol (= fc->exp_params->kT / 1000, scoring.cc:69,91). */
+double adx_kT(void);
+/* Free energy (kcal/mol) of one structure under the loaded model. */
+adx_status adx_eval_structure(const adx_params *p, const char *seq, const char *structure,
+                              double *energy_kcal);
+
+/* ------------------------------------------------------------------------
+ * (1) Per-fold layer: one-to-one with the ViennaRNA calls in scoring.cc.
+ * ---------------------------------------------------------------------- */
+typedef struct adx_fold adx_fold;
+/* vrna_md_set_default + vrna_fold_compound(seq, &md, VRNA_OPTION_PF)
+ * (scoring.cc:79-88); with_bppm mirrors md.compute_bpp (scoring.cc:82-83).
+ * The sequence is upper-cased as ViennaRnaFold's constructor does (:28). */
+adx_status adx_fold_create(const adx_params *p, const char *seq, int with_bppm, int device,
+                           adx_fold **out);
+/* vrna_sc_add_hi_motif(fc, seq, fold, energy, VRNA_OPTION_DEFAULT) (:92-100) */
+adx_status adx_fold_add_motif(adx_fold *f, const char *motif_seq, const char *motif_fold,
+                              double energy_kcal);
+/* vrna_constraints_add(fc, db, DB_DEFAULT | DB_ENFORCE_BP) (:61-62) */
+adx_status adx_fold_add_constraint(adx_fold *f, const char *dot_bracket);
+/* vrna_pf(fc, NULL) (:58, :65): ensemble free energy (kcal/mol, float) */
+adx_status adx_fold_pf(adx_fold *f, float *energy_kcal);
+/* fc->exp_matrices->probs[fc->iindx[i] - j] with 1-based i < j (:47-50);
+ * computed on first use with md.compute_bpp (:41-44). */
+adx_status adx_fold_bpp(adx_fold *f, int i, int j, double *prob);
+/* vrna_fold_compound_free (:31-35) */
+void adx_fold_free(adx_fold *f);
+
+/* ------------------------------------------------------------------------
+ * (2) Batched Monte Carlo layer.
+ * ---------------------------------------------------------------------- */
+#define ADX_APO 0
+#define ADX_HOLO 1
+
+typedef struct adx_term {      /* MacrostateProbTerm (scoring.hh:175-192) */
+    int condition;             /* ADX_APO / ADX_HOLO */
+    int macrostate;            /* index into adx_run_desc.macrostates */
+    int favorable;             /* 1 = "<name>", 0 = "not <name>" */
+    double weight;             /* ScoreTerm weight (scoring.hh:160-168) */
+} adx_term;
+
+#define ADX_THERMO_FIXED 0     /* FixedThermostat (sampling.cc:305-321) */
+#define ADX_THERMO_ANNEAL 1    /* AnnealingThermostat (:324-378) */
+#define ADX_THERMO_AUTO 2      /* AutoScalingThermostat (:381-410) */
+
+typedef struct adx_thermostat {
+    int kind;
+    double t_fixed;
+    double t_hi, t_lo;
+    int cycle_len;
+    double target_rate;
+    int period;
+    double t_init;
+} adx_thermostat;
+
+#define ADX_MOTIF_ADD 0        /* ligand bonus added to the motif structure */
+#define ADX_MOTIF_REPLACE 1    /* motif structure's total energy := bonus */
+
+typedef struct adx_context_desc { /* Context (model.hh:139-157) */
+    const char *before;
+    const char *after;
+} adx_context_desc;
+
+typedef struct adx_run_desc {
+    const adx_params *params;
+    const char *sequence;            /* template Device sequence; upper = mutable */
+    int n_macrostates;
+    const char *const *macrostates;  /* each strlen(sequence) chars */
+    int n_terms;
+    const adx_term *terms;
+    const char *aptamer_seq;         /* NULL: no aptamer (holo folds like apo) */
+    const char *aptamer_fold;
+    double aptamer_energy_kcal;      /* kT*ln(Kd/1M) (scoring.cc:91-99) */
+    int motif_mode;                  /* ADX_MOTIF_ADD / ADX_MOTIF_REPLACE */
+    int n_contexts;                  /* 0 = none; else map (name) order */
+    const adx_context_desc *contexts;
+    adx_thermostat thermostat;
+    int device;                      /* HIP device ordinal */
+} adx_run_desc;
+
+typedef struct adx_ctx adx_ctx;
+
+typedef struct adx_info {
+    int length;          /* N (raw device length) */
+    int n_variants;      /* partition functions per scored step */
+    int n_terms;         /* score terms per context */
+    int n_mutable;       /* freely mutable positions */
+    int max_walkers;
+    double scale_per_nt; /* pf scaling used by the FP32 kernels */
+} adx_info;
+
+adx_status adx_ctx_create(const adx_run_desc *desc, adx_ctx **out);
+void adx_ctx_destroy(adx_ctx *ctx);
+adx_status adx_ctx_info(const adx_ctx *ctx, adx_info *info);
+
+/* W walkers; seqs = W*N chars (NULL: every walker starts from the template),
+ * seeds = W uint32 (std::mt19937(seed) per walker, addapt.cc:89).  Computes
+ * the initial score of each walker (sampling.cc:40). */
+adx_status adx_walkers_init(adx_ctx *ctx, int n_walkers, const char *seqs,
+                            const uint32_t *seeds);
+
+/* Optional per-step trace, host arrays of steps*W entries (step-major). */
+typedef struct adx_trace {
+    int32_t *position;       /* freely-mutable position chosen */
+    char *base;              /* base chosen */
+    int32_t *outcome;        /* 0 REJECT 1 WORSENED 2 UNCHANGED 3 IMPROVED */
+    double *temperature;
+    double *proposed_score;  /* NaN on ACCEPT_UNCHANGED */
+    double *current_score;   /* after the step */
+    double *random_threshold;
+    double *term_values;     /* steps*W*n_terms*max(1,n_contexts), proposed; NaN if unchanged */
+} adx_trace;
+
+/* Advance every walker by `steps` MC steps (fused mutate + fold + score +
+ * Metropolis); the step counter persists across calls (thermostat index). */
+adx_status adx_run_steps(adx_ctx *ctx, int steps, adx_trace *trace);
+
+/* Device time (ms) of the last adx_run_steps / adx_score_batch, measured with
+ * HIP events on the context's stream. */
+adx_status adx_last_kernel_ms(const adx_ctx *ctx, double *ms);
+
+adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
+
+/* Parity entry point: score W sequences (W*N chars) without moving.
+ * scores[W]; term_values[W*n_terms*max(1,n_contexts)] (optional);
+ * dG[W*n_variants] ensemble energies (kcal/mol, float, optional). */
+adx_status adx_score_batch(adx_ctx *ctx, int n_walkers, const char *seqs, double *scores,
+                           double *term_values, float *dG);
+
+/* Variant v of the score: which (context, condition, macrostate or -1). */
+adx_status adx_variant_desc(const adx_ctx *ctx, int v, int *context, int *condition,
+                            int *macrostate);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

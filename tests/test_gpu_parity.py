@@ -1,0 +1,208 @@
+"""GPU parity: the HIP fold/score/MC path against the oracle on the same inputs.
+
+Bar (BASELINE.json north_star): fold free energies within 1e-4 kcal/mol,
+mutation indices / bases bit-exact, Metropolis outcomes identical except at
+near-ties (|crit - u| < 1e-6, resynchronised), scores within the error that
+1e-4 kcal/mol induces in ln p.
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from addapt_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+DG_TOL = 1e-4  # kcal/mol, north_star
+
+
+def rand_seq(rng, n):
+    return "".join(rng.choice("ACGU") for _ in range(n))
+
+
+def rand_constraint(rng, n, p_x=0.1, n_pairs=2):
+    c = ["."] * n
+    for _ in range(n_pairs):
+        i = rng.randrange(0, n - 8)
+        j = rng.randrange(i + 5, n)
+        if all(ch == "." for ch in c[i:j + 1]):
+            c[i], c[j] = "(", ")"
+    for k in range(n):
+        if c[k] == "." and rng.random() < p_x:
+            c[k] = rng.choice("x|<>") if rng.random() < 0.2 else "x"
+    return "".join(c)
+
+
+def test_fold_layer_matches_oracle(native, oracle):
+    rng = random.Random(7)
+    cases = [("ACGUGAAAACGU", None), ("ACGUGAAAACGU", "((((....))))"),
+             ("ACGUGAAAACGU", "xxxx........"), (workloads.THEO_SEQ, None)]
+    for n in (20, 37, 64, 100, 150):
+        for _ in range(3):
+            s = rand_seq(rng, n)
+            cases.append((s, None))
+            cases.append((s, rand_constraint(rng, n)))
+    for seq, cst in cases:
+        f = native.Fold(seq)
+        if cst:
+            f.add_constraint(cst)
+        g = f.pf()
+        ref = np.float32(oracle.pf_energy(seq, cst))
+        if math.isinf(ref):
+            assert math.isinf(g) and g > 0, (seq, cst, g)
+        else:
+            assert abs(g - ref) <= DG_TOL, (seq, cst, g, float(ref))
+
+
+def test_fold_layer_motif(native, oracle):
+    apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
+    e = oracle.theo_bonus()
+    rng = random.Random(3)
+    for seq in (apt, "GGGA" + apt + "UCCC", rand_seq(rng, 20) + apt + rand_seq(rng, 31)):
+        for cst in (None, "." * len(seq)):
+            f = native.Fold(seq)
+            f.add_motif(apt, fold, e)
+            if cst:
+                f.add_constraint(cst)
+            g = f.pf()
+            ref = oracle.pf_energy(seq, cst, oracle.make_motif(apt, fold, e, 0))
+            assert abs(g - np.float32(ref)) <= DG_TOL, (seq, g, ref)
+
+
+def _engine(native, tmpl, macro, terms, aptamer=True, contexts=None, thermostat=None):
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy()) if aptamer else None
+    return native.Engine(tmpl, macro, terms, aptamer=apt, contexts=contexts,
+                         thermostat=thermostat or native.make_thermostat("fixed", t=1.0))
+
+
+def _oracle_sf(oracle, terms, aptamer=True, contexts=None):
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0) if aptamer else None
+    return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts)
+
+
+@pytest.mark.parametrize("N", [60, 100, 150])
+def test_score_batch_synthetic(native, oracle, N):
+    tmpl, active = workloads.synthetic(N)
+    terms = workloads.default_objective()
+    eng = _engine(native, tmpl, [active], terms)
+    seqs = workloads.walker_sequences(tmpl, [active], 16)
+    sc, tv, dg = eng.score_batch(seqs)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in (0, 5, 15):
+            ref = oracle.pf_energy(seqs[w], active if mac >= 0 else None, motif if cond == 1 else None)
+            assert abs(dg[w, v] - np.float32(ref)) <= DG_TOL, (N, v, w, dg[w, v], ref)
+    sf = _oracle_sf(oracle, terms)
+    for w in range(16):
+        ref, tref = sf.score(seqs[w], [active])
+        assert abs(sc[w] - ref) <= 2e-3, (w, sc[w], ref)
+        assert np.allclose(tv[w], tref, atol=2e-3)
+
+
+def test_score_batch_rhf6(native, oracle):
+    terms = workloads.default_objective()
+    eng = _engine(native, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], terms)
+    sc, tv, dg = eng.score_batch([workloads.RHF6_SEQ])
+    ref, tref = _oracle_sf(oracle, terms).score(workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE])
+    assert abs(sc[0] - ref) <= 2e-3
+    # reference thresholds (test_scoring.cc:257-258): holo active prob > 4e-3
+    p_holo = math.exp(tv[0][1])
+    assert p_holo > 4e-3
+
+
+def test_score_batch_contexts_and_terms(native, oracle):
+    tmpl, active = workloads.synthetic(80)
+    other = "." * 10 + "(" + "." * 20 + ")" + "." * (80 - 32)
+    terms = [("apo", 0, False, 1.0), ("holo", 0, True, 0.5), ("apo", 1, True, 2.0)]
+    ctx = [("GGAC", "UUA"), ("", "CCCA"), ("AUAUAU", "")]
+    eng = _engine(native, tmpl, [active, other], terms, contexts=ctx)
+    seqs = workloads.walker_sequences(tmpl, [active, other], 4)
+    sc, tv, _ = eng.score_batch(seqs)
+    sf = _oracle_sf(oracle, terms, contexts=ctx)
+    for w in range(4):
+        ref, tref = sf.score(seqs[w], [active, other])
+        assert abs(sc[w] - ref) <= 5e-3, (w, sc[w], ref)
+        assert np.allclose(tv[w], tref, atol=2e-3)
+
+
+def _replay(oracle, native, eng, tmpl, macro, terms, therm_o, seeds, seqs, steps, aptamer=True):
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms, aptamer)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], macro, therm_o, seed, steps, forced=forced, tie_eps=1e-6)
+        assert ref["rc"] == 0
+        # mutation indices and bases: bit-exact
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert tr["base"][w::len(seeds)] == ref["base"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                assert abs(tr["proposed_score"][s, w] - ref["proposed_score"][s]) <= 2e-3
+                assert tr["random_threshold"][s, w] == ref["random_threshold"][s]
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert abs(scores[w] - ref["score"]) <= 2e-3
+        assert list(counters[w]) == ref["counters"]
+
+
+def test_mc_trajectory_matches_oracle(native, oracle):
+    tmpl, active = workloads.synthetic(60)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [0, 1, 2, 3, 4, 5]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    _replay(oracle, native, eng, tmpl, [active], terms, therm_o, seeds, seqs, 40)
+
+
+def test_mc_trajectory_auto_thermostat(native, oracle):
+    tmpl, active = workloads.synthetic(60)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("auto", rate=0.5, period=7, t0=2.0)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [11, 12]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("auto", rate=0.5, period=7, t0=2.0)
+    _replay(oracle, native, eng, tmpl, [active], terms, therm_o, seeds, seqs, 30)
+
+
+def test_mc_rhf6_single_walker(native, oracle):
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], terms, thermostat=th)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    _replay(oracle, native, eng, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], terms, therm_o, [0],
+            [workloads.RHF6_SEQ], 25)
+
+
+def test_mc_large_batch_invariants(native, oracle):
+    """Full-size config (4096 walkers, N=100): size-independent properties --
+    counters sum to steps, every final score equals the oracle's score of the
+    final sequence, frozen positions and enforced-pair complementarity hold."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    W = 4096
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(2)
+    final, scores, counters = eng.download()
+    assert (counters.sum(axis=1) == 2).all()
+    sf = _oracle_sf(oracle, terms)
+    comp = {"A": "U", "U": "A", "G": "C", "C": "G"}
+    for w in list(range(0, W, 511)) + [W - 1]:
+        s = final[w]
+        for i, c in enumerate(tmpl):
+            if c.islower():
+                assert s[i] == c
+        for k in range(6):
+            assert s[len(s) - 1 - k] == comp[s[k]]
+        ref, _ = sf.score(s, [active])
+        assert abs(scores[w] - ref) <= 2e-3

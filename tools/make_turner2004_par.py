@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Author the nearest-neighbour energy-parameter file used by addapt-amd.
+
+The reference (kalekundert/addapt) folds with ViennaRNA 2.x and its default
+Turner-2004 parameter set (``vrna_md_set_default``, called at
+``/root/reference/src/scoring.cc:81``).  Neither ViennaRNA nor its
+``rna_turner2004.par`` is present in this container and there is no network,
+so this script *authors* a complete parameter set from the Turner-2004 rules
+as known offline:
+
+* values recalled with confidence are written literally (stacking table,
+  loop-length tables, multiloop/ninio/terminal-AU scalars, special hairpins,
+  dangles);
+* the large mismatch / small-interior-loop tables (``mismatch_*``, ``int11``,
+  ``int21``, ``int22``) are generated from the NNDB-2004 rules (AU/GU closure
+  penalty, first-mismatch bonuses, tandem-mismatch bonuses) instead of being
+  copied from ViennaRNA's tables, which are not available here.
+
+The output is written in the ViennaRNA 2.0 parameter-file layout (the layout
+``read_parameter_file`` consumes), so the real ``rna_turner2004.par`` can be
+dropped in unchanged wherever this file is used.  Exact ViennaRNA parity of
+the *values* is therefore "unpinned" (see DESIGN.md §Parity); the binding
+GPU <-> oracle contract is independent of the values.
+
+Usage:  python tools/make_turner2004_par.py > addapt_amd/data/rna_turner2004_addapt.par
+"""
+import sys
+
+INF = 10000000
+PAIRS = ["CG", "GC", "GU", "UG", "AU", "UA", "NS"]   # ViennaRNA pair types 1..7
+BASES = "NACGU"                                         # ViennaRNA base codes 0..4
+RTYPE = {0: 1, 1: 0, 2: 3, 3: 2, 4: 5, 5: 4, 6: 6}      # index (0-based) of reversed pair
+
+
+def au(t):
+    """1 if pair type index t (0-based) is AU/UA/GU/UG (ViennaRNA type > 2)."""
+    return 1 if t >= 2 else 0
+
+
+# --- literal tables (dcal/mol) -------------------------------------------------
+STACK = [
+    [-240, -330, -210, -140, -210, -210],
+    [-330, -340, -250, -150, -220, -240],
+    [-210, -250, 130, -50, -140, -130],
+    [-140, -150, -50, 30, -60, -100],
+    [-210, -220, -140, -60, -110, -90],
+    [-210, -240, -130, -100, -90, -130],
+]
+# dangle5[type][base]: base 5' of the pair's 5' nucleotide; dangle3: 3' of the 3' nucleotide
+D5 = {  # A, C, G, U
+    "CG": [-50, -30, -20, -10], "GC": [-20, -30, 0, 0], "GU": [-30, -30, -40, -20],
+    "UG": [-30, -10, -20, -20], "AU": [-30, -30, -40, -20], "UA": [-30, -10, -20, -20],
+}
+D3 = {
+    "CG": [-110, -40, -130, -60], "GC": [-170, -80, -170, -120], "GU": [-70, -10, -70, -10],
+    "UG": [-80, -50, -80, -60], "AU": [-70, -10, -70, -10], "UA": [-80, -50, -80, -60],
+}
+HAIRPIN = [INF, INF, INF, 540, 560, 570, 540, 600, 550, 640, 650, 660, 670, 678, 686, 694,
+           701, 707, 713, 719, 725, 730, 735, 740, 744, 749, 753, 757, 761, 765, 769]
+BULGE = [INF, 380, 280, 320, 360, 400, 440, 459, 470, 480, 490, 500, 510, 519, 527, 534,
+         541, 548, 554, 560, 565, 571, 576, 580, 585, 589, 594, 598, 602, 605, 609]
+INTERIOR = [INF, INF, INF, INF, 110, 200, 200, 210, 230, 240, 250, 260, 270, 280, 290, 290,
+            300, 310, 310, 320, 330, 330, 340, 340, 350, 350, 350, 360, 360, 370, 370]
+TETRALOOPS = [("CAACGG", 550), ("CCAAGG", 330), ("CCACGG", 370), ("CCCAGG", 340),
+              ("CCGAGG", 350), ("CCGCGG", 360), ("CCUAGG", 370), ("CCUCGG", 250),
+              ("CUAAGG", 360), ("CUACGG", 280), ("CUCAGG", 370), ("CUCCGG", 270),
+              ("CUGCGG", 280), ("CUUAGG", 350), ("CUUCGG", 370), ("CUUUGG", 370)]
+TRILOOPS = [("CAACG", 680), ("GUUAC", 690)]
+HEXALOOPS = [("ACAGUACU", 280), ("ACAGUGAU", 360), ("ACAGUGCU", 290), ("ACAGUGUU", 180)]
+ML_BASE, ML_CLOSING, ML_INTERN = 0, 930, -90
+NINIO, MAX_NINIO = 60, 300
+DUPLEX_INIT, TERMINAL_AU, LXC = 410, 50, 107.856
+
+# --- rule-generated tables ----------------------------------------------------
+def b(c):
+    return BASES.index(c)
+
+
+def dangle(table, t, x):
+    """dangle value for pair index t (0..5) and base code x (1..4); N (0) -> max."""
+    row = table[PAIRS[t]]
+    return max(row) if x == 0 else row[x - 1]
+
+
+def mm_hairpin(t, x, y):
+    # terminal mismatch seen from inside the loop = 3'-dangle of x + 5'-dangle of y on
+    # the reversed pair, plus the Turner-2004 first-mismatch bonuses (UU, GA, GG).
+    rt = RTYPE[t]
+    e = dangle(D3, rt, x) + dangle(D5, rt, y)
+    if x == b("U") and y == b("U"):
+        e -= 90
+    elif x == b("G") and y == b("A"):
+        e -= 80
+    elif x == b("G") and y == b("G"):
+        e -= 80
+    return e
+
+
+def first_mismatch_interior(x, y):
+    if x == b("U") and y == b("U"):
+        return -70
+    if x == b("G") and y == b("A"):
+        return -110
+    if x == b("A") and y == b("G"):
+        return -80
+    return 0
+
+
+def mm_interior(t, x, y):
+    return 70 * au(t) + first_mismatch_interior(x, y)
+
+
+def mm_interior_1n(t, x, y):
+    return 70 * au(t)
+
+
+def mm_interior_23(t, x, y):
+    return 70 * au(t) + first_mismatch_interior(x, y)
+
+
+def mm_exterior(t, x, y):
+    # dangles=2 convention: a stem sees both neighbours; mismatch = d5 + d3
+    return dangle(D5, t, x) + dangle(D3, t, y)
+
+
+def tandem(x, y):
+    if (x, y) in ((b("G"), b("A")), (b("A"), b("G"))):
+        return -60
+    if x == b("U") and y == b("U"):
+        return -40
+    if x == b("G") and y == b("G"):
+        return -50
+    return 0
+
+
+def int11(t1, t2, x, y):
+    e = 50 + 70 * au(t1) + 70 * au(t2)
+    if x == b("G") and y == b("G"):
+        e -= 170
+    return e
+
+
+def int21(t1, t2, x, y, z):
+    return 230 + 70 * au(t1) + 70 * au(t2)
+
+
+def int22(t1, t2, a, bb, c, d):
+    # a = S[i+1], bb = S[p-1], c = S[q+1], d = S[j-1]
+    return 120 + 70 * au(t1) + 70 * au(t2) + tandem(a, d) + tandem(c, bb)
+
+
+# --- writer -------------------------------------------------------------------
+def fmt(v):
+    if v >= INF:
+        return "   INF"
+    return "%6d" % v
+
+
+def row(vals):
+    return " ".join(fmt(v) for v in vals)
+
+
+def ns_fill(fn, dims):
+    """Value for entries touching the non-standard pair type: the max over canonical types."""
+    return fn
+
+
+def mismatch_section(name, fn):
+    out = ["# " + name]
+    for t in range(7):
+        out.append("/* %s */" % PAIRS[t])
+        for x in range(5):
+            vals = []
+            for y in range(5):
+                if t == 6:
+                    vals.append(max(fn(tt, x, y) for tt in range(6)))
+                else:
+                    vals.append(fn(t, x, y))
+            out.append(row(vals))
+    return out
+
+
+def main():
+    o = []
+    o.append("## RNAfold parameter file v2.0")
+    o.append("")
+    o.append("/* addapt-amd: Turner-2004-derived parameter set authored offline by")
+    o.append("   tools/make_turner2004_par.py (see its docstring). ViennaRNA 2.0 layout;")
+    o.append("   the real rna_turner2004.par can be used instead. */")
+    o.append("")
+    o.append("# stack")
+    o.append("/*  CG     GC     GU     UG     AU     UA     @ */")
+    for t in range(7):
+        vals = []
+        for t2 in range(7):
+            if t < 6 and t2 < 6:
+                vals.append(STACK[t][t2])
+            else:
+                vals.append(max(STACK[a][c] for a in range(6) for c in range(6)))
+        o.append(row(vals))
+    o.append("")
+    o += mismatch_section("mismatch_hairpin", mm_hairpin)
+    o.append("")
+    o += mismatch_section("mismatch_interior", mm_interior)
+    o.append("")
+    o += mismatch_section("mismatch_interior_1n", mm_interior_1n)
+    o.append("")
+    o += mismatch_section("mismatch_interior_23", mm_interior_23)
+    o.append("")
+    o += mismatch_section("mismatch_multi", mm_exterior)
+    o.append("")
+    o += mismatch_section("mismatch_exterior", mm_exterior)
+    o.append("")
+    for name, tab in (("dangle5", D5), ("dangle3", D3)):
+        o.append("# " + name)
+        o.append("/*  @     A     C     G     U */")
+        for t in range(7):
+            if t == 6:
+                vals = [max(max(tab[p]) for p in PAIRS[:6])] + \
+                       [max(tab[p][k] for p in PAIRS[:6]) for k in range(4)]
+            else:
+                vals = [max(tab[PAIRS[t]])] + tab[PAIRS[t]]
+            o.append(row(vals))
+        o.append("")
+    # int11: 7x7 blocks of 5x5
+    o.append("# int11")
+    for t1 in range(7):
+        for t2 in range(7):
+            o.append("/* %s..%s */" % (PAIRS[t1], PAIRS[t2]))
+            for x in range(5):
+                vals = []
+                for y in range(5):
+                    if t1 == 6 or t2 == 6 or x == 0 or y == 0:
+                        vals.append(int11(min(t1, 5), min(t2, 5), 1, 1) + 100)
+                    else:
+                        vals.append(int11(t1, t2, x, y))
+                o.append(row(vals))
+    o.append("")
+    # int21: 7x7x5 blocks of 5x5
+    o.append("# int21")
+    for t1 in range(7):
+        for t2 in range(7):
+            for x in range(5):
+                o.append("/* %s.%s..%s */" % (PAIRS[t1], BASES[x], PAIRS[t2]))
+                for y in range(5):
+                    vals = []
+                    for z in range(5):
+                        if t1 == 6 or t2 == 6 or 0 in (x, y, z):
+                            vals.append(int21(min(t1, 5), min(t2, 5), 1, 1, 1) + 100)
+                        else:
+                            vals.append(int21(t1, t2, x, y, z))
+                    o.append(row(vals))
+    o.append("")
+    # int22: 6x6 canonical types, 4x4x4 blocks of 4 (bases A..U)
+    o.append("# int22")
+    for t1 in range(6):
+        for t2 in range(6):
+            for a in range(1, 5):
+                for bb in range(1, 5):
+                    o.append("/* %s.%s%s..%s */" % (PAIRS[t1], BASES[a], BASES[bb], PAIRS[t2]))
+                    for c in range(1, 5):
+                        o.append(row([int22(t1, t2, a, bb, c, d) for d in range(1, 5)]))
+    o.append("")
+    for name, tab in (("hairpin", HAIRPIN), ("bulge", BULGE), ("interior", INTERIOR)):
+        o.append("# " + name)
+        o.append(row(tab[:10]))
+        o.append(row(tab[10:20]))
+        o.append(row(tab[20:]))
+        o.append("")
+    o.append("# ML_params")
+    o.append("/* F = cu*n_unpaired + cc + ci*loop_degree (branches) */")
+    o.append("/*\t    cu\t    cu_dH\t    cc\t    cc_dH\t    ci\t    ci_dH  */")
+    o.append("%6d %6d %6d %6d %6d %6d" % (ML_BASE, 0, ML_CLOSING, 3000, ML_INTERN, -220))
+    o.append("")
+    o.append("# NINIO")
+    o.append("/* Ninio = MIN(max, m*|n1-n2| */")
+    o.append("/*\t    m\t  m_dH     max  */")
+    o.append("%6d %6d %6d" % (NINIO, 320, MAX_NINIO))
+    o.append("")
+    o.append("# Misc")
+    o.append("/* all parameters are pairs of 'energy enthalpy' */")
+    o.append("/*    DuplexInit     TerminalAU      LXC */")
+    o.append("%6d %6d %6d %6d %10.6f %6d" % (DUPLEX_INIT, 360, TERMINAL_AU, 370, LXC, 0))
+    o.append("")
+    for name, tab in (("Triloops", TRILOOPS), ("Tetraloops", TETRALOOPS), ("Hexaloops", HEXALOOPS)):
+        o.append("# " + name)
+        for s, e in tab:
+            o.append("%s %6d %6d" % (s, e, 0))
+        o.append("")
+    o.append("# END")
+    sys.stdout.write("\n".join(o) + "\n")
+
+
+if __name__ == "__main__":
+    main()
