@@ -173,47 +173,44 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
                   const std::vector<int> &mpt, DevScaled &X) {
     std::memset(&X, 0, sizeof X);
     auto sp = [&](int k) { return std::pow(sigma, k); };
-    int n = 0;
-    for (int u = 0; u <= MAXLOOP; u++) {
-        for (int n1 = 0; n1 <= u; n1++) {
-            const int n2 = u - n1;
-            const int nl = std::max(n1, n2), ns = std::min(n1, n2);
-            TermDesc t;
-            t.n1 = static_cast<uint8_t>(n1);
-            t.n2 = static_cast<uint8_t>(n2);
-            t.u = static_cast<uint8_t>(u);
-            double f;
-            if (u == 0) {
-                t.kind = K_STACK;
-                f = 1.0;
-            } else if (ns == 0) {
-                t.kind = (nl == 1) ? K_BULGE1 : K_BULGE;
-                f = boltz_d(P.bulge[nl]);
-            } else if (ns == 1 && nl == 1) {
-                t.kind = K_I11;
-                f = 1.0;
-            } else if (ns == 1 && nl == 2) {
-                t.kind = (n1 == 1) ? K_I21 : K_I12;
-                f = 1.0;
-            } else if (ns == 1) {
-                t.kind = K_1N;
-                f = boltz_d(P.interior[nl + 1] + std::min(P.maxninio, (nl - ns) * P.ninio));
-            } else if (ns == 2 && nl == 2) {
-                t.kind = K_I22;
-                f = 1.0;
-            } else if (ns == 2 && nl == 3) {
-                t.kind = K_I23;
-                f = boltz_d(P.interior[5] + P.ninio);
-            } else {
-                t.kind = K_GENERIC;
-                f = boltz_d(P.interior[u] + std::min(P.maxninio, (nl - ns) * P.ninio));
-            }
-            t.f = static_cast<float>(f * sp(u + 2));
-            X.terms[n++] = t;
-        }
-        X.ncnt[u] = n;
+    float *ct = X.ctab;
+    // code = rtype*25 + S[q+1]*5 + S[p-1] of an inner pair; mismatchI[type2][sq1][sp1]
+    for (int code = 0; code < 200; code++) {
+        const int t2 = code / 25, x = (code / 5) % 5, y = code % 5;
+        const double mm = t2 ? boltz_d(P.mmI[t2][x][y]) : 0.0;
+        const double inv = (mm > 0.0) ? 1.0 / mm : 0.0;
+        ct[CT_INVMM + code] = static_cast<float>(inv);
+        ct[CT_BUL + code] = static_cast<float>(inv * (t2 ? boltz_d(t2 > 2 ? P.TermAU : 0) : 0.0));
+        ct[CT_ONEN + code] = static_cast<float>(inv * (t2 ? boltz_d(P.mm1nI[t2][x][y]) : 0.0));
+        ct[CT_M23O + code] = static_cast<float>(t2 ? boltz_d(P.mm23I[t2][x][y]) : 0.0);
     }
-    X.ncnt[31] = n;
+    for (int a = 0; a < 8; a++)
+        for (int b = 0; b < 8; b++) ct[CT_STK + a * 8 + b] = (a && b) ? boltz(P.stack[a][b]) : 0.f;
+    for (int u = 0; u < 32; u++) {
+        const int uu = std::min(u, MAXLOOP);
+        ct[CT_FB + u] = static_cast<float>(boltz_d(P.bulge[uu]) * sp(u + 2));
+        const int nl = u;
+        const double e1n = (nl >= 1 && nl + 1 <= MAXLOOP)
+                               ? P.interior[nl + 1] + std::min(P.maxninio, (nl - 1) * P.ninio)
+                               : INF_E;
+        ct[CT_F1N + u] = static_cast<float>(boltz_d(e1n) * sp(nl + 3));
+    }
+    ct[CT_FSM + 0] = static_cast<float>(sp(2));
+    ct[CT_FSM + 1] = static_cast<float>(boltz_d(P.bulge[1]) * sp(3));
+    ct[CT_FSM + 2] = static_cast<float>(sp(4));
+    ct[CT_FSM + 3] = static_cast<float>(sp(5));
+    ct[CT_FSM + 4] = static_cast<float>(sp(6));
+    ct[CT_FSM + 5] = static_cast<float>(boltz_d(P.interior[5] + P.ninio) * sp(7));
+    ct[CT_FSM + 6] = static_cast<float>(boltz_d(P.TermAU));
+    ct[CT_FSM + 7] = 0.f;
+    for (int u = 6; u <= MAXLOOP; u++)
+        for (int n1 = 2; n1 < 2 + FG_ROW; n1++) {
+            const int n2 = u - n1;
+            double f = 0.0;
+            if (n2 >= 2)
+                f = boltz_d(P.interior[u] + std::min(P.maxninio, std::abs(n1 - n2) * P.ninio)) * sp(u + 2);
+            X.fgen[(u - 6) * FG_ROW + n1 - 2] = static_cast<float>(f);
+        }
     for (int k = 0; k < NMAX + 4; k++) X.sig[k] = static_cast<float>(sp(k));
     for (int u = 0; u <= NMAX; u++) {
         double e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + P.lxc * std::log(u / 30.0);
@@ -594,6 +591,9 @@ struct adx_ctx {
     DevBuf<uint32_t> mtA, mtC;
     DevBuf<int64_t> counters;
     DevBuf<int> ntrain, err;
+    DevBuf<uint8_t> prop_seq;
+    DevBuf<double> prop_score, temp, u;
+    DevBuf<int> changed, pick, bcode;
     DevBuf<int> d_mut, d_clo_off, d_clo_pos, d_clo_err;
     DevBuf<uint8_t> d_clo_par;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -851,6 +851,13 @@ extern "C" adx_status adx_walkers_init(adx_ctx *c, int W, const char *seqs, cons
     HIP_TRY(c->counters.alloc(size_t(W) * 4));
     HIP_TRY(c->ntrain.alloc(W));
     HIP_TRY(c->err.alloc(W));
+    HIP_TRY(c->prop_seq.alloc(size_t(W) * N));
+    HIP_TRY(c->prop_score.alloc(W));
+    HIP_TRY(c->temp.alloc(W));
+    HIP_TRY(c->u.alloc(W));
+    HIP_TRY(c->changed.alloc(W));
+    HIP_TRY(c->pick.alloc(W));
+    HIP_TRY(c->bcode.alloc(W));
     const int period = std::max(1, c->thermo.period);
     HIP_TRY(c->train.alloc(c->thermo.kind == ADX_THERMO_AUTO ? size_t(W) * period : 1));
     HIP_TRY(hipMemsetAsync(c->last_diff.p, 0, sizeof(double) * W, pb.stream));
@@ -882,6 +889,14 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     st.train = c->train.p;
     st.ntrain = c->ntrain.p;
     st.err = c->err.p;
+    st.prop_seq = c->prop_seq.p;
+    st.prop_score = c->prop_score.p;
+    st.changed = c->changed.p;
+    st.pick = c->pick.p;
+    st.bcode = c->bcode.p;
+    st.temp = c->temp.p;
+    st.u = c->u.p;
+    st.Nraw = pb.Nraw;
     st.mut = c->d_mut.p;
     st.clo_off = c->d_clo_off.p;
     st.clo_pos = c->d_clo_pos.p;

@@ -17,28 +17,27 @@ namespace adx {
 constexpr int NMAX = 255;          // positions (u8 indices in LDS lists)
 constexpr int MAX_VARIANTS = 64;
 constexpr int MAX_TERMS = 64;
-constexpr int MAX_SPECIAL_HP = 96;
+constexpr int MAX_SPECIAL_HP = 64;
 constexpr int MAX_MOTIF = 96;
-constexpr int N_INT_TERMS = 496;   // (n1, n2) with n1 + n2 <= 30
 constexpr int MT_WORDS = 625;      // 624 state words + index
 
-enum TermKind : uint8_t {
-    K_GENERIC = 0,
-    K_STACK = 1,
-    K_BULGE1 = 2,
-    K_BULGE = 3,
-    K_I11 = 4,
-    K_I21 = 5,   // n1 = 1, n2 = 2
-    K_I12 = 6,   // n1 = 2, n2 = 1
-    K_I22 = 7,
-    K_I23 = 8,   // 2x3 and 3x2
-    K_1N = 9,    // 1xn and nx1, n >= 3
-};
-
-struct TermDesc {          // one interior-loop shape, sorted by u = n1 + n2
-    uint8_t n1, n2, kind, u;
-    float f;               // shape-only Boltzmann factor * sigma^(u+2)
-};
+// Per-context factor table copied into LDS by every workgroup
+// (DevScaled::ctab).  "code" = the inner-pair code of a DP cell (p,q):
+// rtype(p,q)*25 + S[q+1]*5 + S[p-1] (< 200), stored per cell in LDS; qbm
+// holds qb * mismatchI[code], so qb = qbm * CT_INVMM[code].
+constexpr int CT_INVMM = 0;    // [code] 1 / exp(-mismatchI)
+constexpr int CT_BUL = 200;    // [code] INVMM * TermAU factor of the inner pair (bulges n >= 2)
+constexpr int CT_ONEN = 400;   // [code] INVMM * exp(-mismatch_interior_1n)
+constexpr int CT_M23O = 600;   // [code] exp(-mismatch_interior_23)
+constexpr int CT_STK = 800;    // [8][8] stack
+constexpr int CT_FB = 864;     // [n]   bulge n: exp(-bulge[n]) * sigma^(n+2)
+constexpr int CT_F1N = 896;    // [nl]  1 x nl: exp(-(interior[nl+1] + ninio)) * sigma^(nl+3)
+constexpr int CT_FSM = 928;    // [0] s^2 [1] bulge1 s^3 [2] s^4 [3] s^5 [4] s^6 [5] 2x3 s^7 [6] exp(-TermAU)
+constexpr int CT_SIZE = 936;
+// generic interior factors exp(-(interior[u] + ninio)) * sigma^(u+2) for
+// u = 6..30, n1 = 2..28: DevScaled::fgen[(u - 6) * FG_ROW + n1 - 2]
+constexpr int FG_ROW = 27;
+constexpr int FG_SIZE = 25 * FG_ROW;
 
 struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
     float stack[8][8];
@@ -55,8 +54,8 @@ struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
 };
 
 struct DevScaled {
-    TermDesc terms[N_INT_TERMS];
-    int ncnt[32];            // number of terms with u <= k
+    float ctab[CT_SIZE];     // see CT_* (copied to LDS)
+    float fgen[FG_SIZE];     // generic interior factors (copied to LDS)
     float sig[NMAX + 4];     // sigma^k
     float hp[NMAX + 1];      // hairpin length factor * sigma^(u+2)
     float pwml[NMAX + 1];    // (expMLbase * sigma)^t
@@ -123,6 +122,12 @@ struct StepArgs {
     double *train;              // W * period
     int *ntrain;                // W
     int *err;                   // W (0 ok, else move error code)
+    uint8_t *prop_seq;          // W * Nraw proposal
+    double *prop_score;         // W
+    int *changed;               // W (1 = scored this step)
+    int *pick, *bcode;          // W
+    double *temp, *u;           // W
+    int Nraw;
     const int *mut;             // freely mutable positions (0-based raw), M
     const int *clo_off;         // M + 1
     const int *clo_pos;         // closure positions (0-based raw)

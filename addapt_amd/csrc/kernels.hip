@@ -30,47 +30,97 @@
 
 namespace adx {
 
+#ifdef ADX_STAMP
+// Diagnostic build only: per-wave cycle sums of the per-diagonal phases
+// (s_memtime), read back through adx_debug_stamps().  Never in the product.
+__device__ unsigned long long g_stamps[16][16];
+#define STAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 namespace {
 
 constexpr int WAVE = 64;
-
-__device__ __constant__ int8_t PAIR_D[5][5] = {{0, 0, 0, 0, 0},
-                                               {0, 0, 0, 0, 5},
-                                               {0, 0, 0, 1, 0},
-                                               {0, 0, 2, 0, 3},
-                                               {0, 6, 0, 4, 0}};
-__device__ __constant__ int8_t RTYPE_D[8] = {0, 2, 1, 4, 3, 6, 5, 7};
-
-__device__ __forceinline__ int ptype(int a, int b) { return PAIR_D[a][b]; }
 
 // index of the first cell of diagonal dd (cells with j - i = dd >= 4)
 __device__ __forceinline__ int off(int dd, int N) { return ((dd - 4) * (2 * N - 3 - dd)) >> 1; }
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+// Full-wave sum via DPP (quad_perm, row_shr, row_bcast): VALU-only, no LDS
+// crossbar; the total lands in lane 63 and is read back with readlane.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_add(float v) {
+    const int moved = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false);
+    return v + __int_as_float(moved);
 }
+__device__ __forceinline__ float wave_sum(float v) {
+    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15
+    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// Pair type / reversed type / terminal-AU flag without a memory lookup:
+// PAIR[a][b] for codes a, b in 0..4 (ViennaRNA types 1..6) packed 3 bits per
+// entry of index 5a+b-9 (the canonical pairs sit at 9..23).
+constexpr unsigned long long pack_pairs() {
+    unsigned long long k = 0;
+    k |= 5ull << (3 * (9 - 9));    // A-U
+    k |= 1ull << (3 * (13 - 9));   // C-G
+    k |= 2ull << (3 * (17 - 9));   // G-C
+    k |= 3ull << (3 * (19 - 9));   // G-U
+    k |= 6ull << (3 * (21 - 9));   // U-A
+    k |= 4ull << (3 * (23 - 9));   // U-G
+    return k;
+}
+__device__ __forceinline__ int ptype(int a, int b) {
+    const int idx = 5 * a + b - 9;
+    return (idx >= 0 && idx <= 14) ? int((pack_pairs() >> (3 * idx)) & 7ull) : 0;
+}
+__device__ __forceinline__ int rtype(int t) { return t ? (((t - 1) ^ 1) + 1) : 0; }
+
+// Cell indexing (1-based i < j, span j - i >= 4):
+//   qbm, cc  diagonal-major  off(j-i) + i - 1   (cells of one anti-diagonal contiguous)
+//   qm       row-major       rowb(i) + j - i - 4 (qm[i][*] contiguous)
+//   qm1      column-major    colb(j) + i - 1     (qm1[*][j] contiguous)
+// so every inner loop of the recurrence walks contiguous LDS at a per-lane base.
+__device__ __forceinline__ int rowb(int i, int N) { return (i - 1) * (N - 3) - (((i - 1) * i) >> 1); }
+__device__ __forceinline__ int colb(int j) { return ((j - 5) * (j - 4)) >> 1; }
+
+// LDS per-cell table block (L.dt), copied from DevTables / DevScaled
+constexpr int DT_MMH = 0;      // [type][x][y] hairpin mismatch
+constexpr int DT_MMI = 200;    // [type][x][y] interior mismatch
+constexpr int DT_MLS = 400;    // [type][x][y] multiloop stem
+constexpr int DT_EXT = 600;    // [type][6][6] exterior stem
+constexpr int DT_TAU = 888;    // [type] terminal AU
+constexpr int DT_SPK = 896;    // special hairpin keys (bit patterns)
+constexpr int DT_SPV = DT_SPK + MAX_SPECIAL_HP;
+constexpr int DT_HP = DT_SPV + MAX_SPECIAL_HP;  // [u] hairpin length factor
 
 // LDS carve-out for one workgroup (see lds_bytes()).
 struct Lds {
-    float *qb, *qm, *qm1, *qbm;
-    float *scrA, *scrB, *q5;
+    float *qbm, *qm, *qm1;
+    uint8_t *cc;       // inner-pair code per cell (diagonal-major)
+    float *scr;        // 2 x NT floats (double-buffered partial rows) + 4 q5 partials
+    float *ct;         // CT_SIZE factor table (DevScaled::ctab)
+    float *dt;         // LDS copy of per-cell tables (DT_*)
+    float *q5;
     float *misc;       // [0] = q5 partial
     double *G;         // per-variant ensemble energies
     uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat;
-    uint8_t *lists;    // plist[2] then pinv[2], NP bytes each
+    uint8_t *lists;    // plist[4] then pinv[4], NP bytes each
     int np;
     int *pcount;       // [2]
-    uint8_t *raw;      // proposal / scored sequence (Nraw)
-    uint32_t *rng;     // aliased onto the tables: 2 * MT_WORDS
-    double *dscr;      // scratch doubles (median etc.)
+    uint8_t *raw;      // scored sequence (Nraw)
 };
 
 template <int NT>
-__device__ Lds carve(char *base, const KArgs &ka, bool qbm) {
+__device__ Lds carve(char *base, const KArgs &ka) {
     Lds L;
     const int C = ka.cells;
     size_t o = 0;
@@ -79,20 +129,17 @@ __device__ Lds carve(char *base, const KArgs &ka, bool qbm) {
         o += (bytes + 15) & ~size_t(15);
         return p;
     };
-    const size_t tbytes = size_t(C) * 4 * (qbm ? 4 : 3);
-    char *tb = take(tbytes > 2 * MT_WORDS * 4 ? tbytes : 2 * MT_WORDS * 4);
-    L.qb = reinterpret_cast<float *>(tb);
-    L.qm = L.qb + C;
-    L.qm1 = L.qm + C;
-    L.qbm = qbm ? L.qm1 + C : nullptr;
-    L.rng = reinterpret_cast<uint32_t *>(tb);
-    L.scrA = reinterpret_cast<float *>(take(NT * 4));
-    L.scrB = reinterpret_cast<float *>(take(NT * 4));
+    L.qbm = reinterpret_cast<float *>(take(size_t(C) * 4));
+    L.qm = reinterpret_cast<float *>(take(size_t(C) * 4));
+    L.qm1 = reinterpret_cast<float *>(take(size_t(C) * 4));
+    L.cc = reinterpret_cast<uint8_t *>(take(size_t(C)));
+    L.scr = reinterpret_cast<float *>(take(2 * NT * 4 + 16));
+    L.ct = reinterpret_cast<float *>(take(CT_SIZE * 4));
+    L.dt = reinterpret_cast<float *>(take(size_t(DT_HP + ka.Nmax + 1) * 4));
     const int NP = ka.Nmax + 2;
     L.q5 = reinterpret_cast<float *>(take(NP * 4));
     L.misc = reinterpret_cast<float *>(take(16 * 4));
-    L.G = reinterpret_cast<double *>(take(MAX_VARIANTS * 8));
-    L.dscr = reinterpret_cast<double *>(take(16 * 8));
+    L.G = reinterpret_cast<double *>(take(ka.n_variants * 8));
     L.pcount = reinterpret_cast<int *>(take(4 * 4));
     L.S = reinterpret_cast<uint8_t *>(take(NP));
     L.up = reinterpret_cast<uint8_t *>(take(NP));
@@ -102,13 +149,32 @@ __device__ Lds carve(char *base, const KArgs &ka, bool qbm) {
     L.flg = reinterpret_cast<uint8_t *>(take(NP));
     L.mat = reinterpret_cast<uint8_t *>(take(NP));
     L.np = NP;
-    L.lists = reinterpret_cast<uint8_t *>(take(4 * NP));
+    L.lists = reinterpret_cast<uint8_t *>(take(8 * NP));
     L.raw = reinterpret_cast<uint8_t *>(take(NP));
     return L;
 }
 
+template <int NT>
+__device__ void load_ctab(const KArgs &ka, const Lds &L) {
+    for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = ka.X->ctab[k];
+    const DevTables &T = *ka.T;
+    const DevScaled &X = *ka.X;
+    for (int k = threadIdx.x; k < 200; k += NT) {
+        L.dt[DT_MMH + k] = (&T.mmH[0][0][0])[k];
+        L.dt[DT_MMI + k] = (&T.mmI[0][0][0])[k];
+        L.dt[DT_MLS + k] = (&T.mlstem[0][0][0])[k];
+    }
+    for (int k = threadIdx.x; k < 288; k += NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
+    for (int k = threadIdx.x; k < 8; k += NT) L.dt[DT_TAU + k] = T.termAU[k];
+    for (int k = threadIdx.x; k < MAX_SPECIAL_HP; k += NT) {
+        L.dt[DT_SPK + k] = __uint_as_float(k < X.n_special ? X.sp_key[k] : 0u);
+        L.dt[DT_SPV + k] = X.sp_val[k];
+    }
+    for (int k = threadIdx.x; k <= ka.Nmax; k += NT) L.dt[DT_HP + k] = X.hp[k];
+}
+
 __device__ __forceinline__ uint8_t *plist(const Lds &L, int b) { return L.lists + b * L.np; }
-__device__ __forceinline__ uint8_t *pinv(const Lds &L, int b) { return L.lists + (2 + b) * L.np; }
+__device__ __forceinline__ uint8_t *pinv(const Lds &L, int b) { return L.lists + (4 + b) * L.np; }
 
 // ---------------------------------------------------------------- hard constraints
 // flg bits: 1 = 'x' (no pair), 2 = '<' (pairs upstream), 4 = '>' (downstream);
@@ -127,7 +193,7 @@ __device__ __forceinline__ bool pairable(const Lds &L, int i, int j) {
     return ptype(L.S[i], L.S[j]) != 0 && allowed(L, i, j);
 }
 
-// wave 0: compact the pairable cells of diagonal dd into buffer b
+// one wave: compact the pairable cells of diagonal dd into buffer b
 __device__ void build_plist(const Lds &L, int N, int dd, int b, int lane) {
     const int c = N - dd;
     int base = 0;
@@ -150,15 +216,24 @@ __device__ void build_plist(const Lds &L, int N, int dd, int b, int lane) {
 }
 
 // ---------------------------------------------------------------- inside PF
-// Returns the ensemble free energy (kcal/mol, double) of variant v folded on
-// the raw sequence `raw` (codes, Nraw); all threads of the block must call.
-template <int NT, bool QBM>
-__device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds &L) {
+// Per-diagonal pipeline with ONE barrier per iteration d:
+//   jobs (all waves, lanes = cells):  A  qb(d) partials      (reads spans <= d-2)
+//                                     B  qm(d-2) partials    (qm1 span d-2, qm <= d-7)
+//                                     C  q5[d-1] partial     (qb spans <= d-2)
+//   finalize (one item per thread):   qb(d-1) + qbm/code + qm1(d-1), qm(d-3), q5[d-2],
+//                                     from the partials iteration d-1 left in the other
+//                                     scratch buffer; plus the pairable list of d+1.
+// qb(d) never reads span d-1 (stack = span d-2), so the finalize of d-1 and the
+// partials of d share one phase.
+template <int NT>
+__device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds &L,
+                           const DevScaled *__restrict__ XS) {
     constexpr int NW = NT / WAVE;
     const DevVariant V = ka.variants[v];
     const int N = V.N;
     const DevTables &T = *ka.T;
     const DevScaled &X = *ka.X;
+    const float *ct = L.ct;
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int wid = uni(tid / WAVE);
@@ -167,13 +242,13 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
     const uint8_t *cons = ka.cons + V.cons_off;
     const int np = N + 2;
     const uint8_t *bef = nullptr, *aft = nullptr;
-    int blen = 0, alen = 0;
+    int blen = 0;
     if (V.ctx >= 0) {
         bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
         blen = ka.ctx_off[4 * V.ctx + 1];
         aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
-        alen = ka.ctx_off[4 * V.ctx + 3];
     }
+    bool constrained = false;
     for (int k = tid; k < np; k += NT) {
         uint8_t s = 0;
         if (k >= 1 && k <= N) {
@@ -183,18 +258,21 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
             else s = aft[p - blen - ka.Nraw];
         }
         L.S[k] = s;
+        const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k];
         L.up[k] = cons[k];
         L.dn[k] = cons[np + k];
-        L.ptn[k] = cons[2 * np + k];
+        L.ptn[k] = pt;
         L.enc[k] = cons[3 * np + k];
-        L.flg[k] = cons[4 * np + k];
+        L.flg[k] = f;
         L.mat[k] = 0;
+        if (k >= 1 && k <= N && (f || pt)) constrained = true;
     }
-    __syncthreads();
+    constrained = __syncthreads_or(constrained);
     if (tid == 0) {
         // ViennaRNA's S1 wrap-around (only reaches values that are never used)
         L.S[0] = L.S[N];
         L.S[N + 1] = L.S[1];
+        L.q5[0] = 1.0f;
     }
     const int mL = X.motif_len;
     if (V.motif && mL > 0) {
@@ -211,185 +289,395 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
             L.mat[o] = ok ? 1 : 0;
         }
     }
-    if (tid < 4) {
-        if (tid == 0) L.q5[0] = 1.0f;
-    }
     __syncthreads();
-    if (tid == 0) {
-        for (int j = 1; j <= 3 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] * X.sig[1] : 0.f;
-    }
-    if (wid == 0 && N - 1 >= 4) build_plist(L, N, 4, 0, lane);
-    __syncthreads();
-
     const float sig1 = X.sig[1];
+    if (tid == 0) {
+        for (int j = 1; j <= 3 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] * sig1 : 0.f;
+    }
+    if (wid == NW - 1 && N - 1 >= 4) build_plist(L, N, 4, 0, lane);
+    __syncthreads();
+
     const float mlbase_sig = X.mlbase_sig;
+    const float mlclosing = X.mlclosing;
+    const float eTAU = ct[CT_FSM + 6];
+    const int mlen = V.motif ? mL : 0;
+    const float mextra = X.motif_extra;
+    const int nsp = X.n_special < MAX_SPECIAL_HP ? X.n_special : MAX_SPECIAL_HP;
+    // split of the previous iteration (to find its partials)
+    int p_gA = 0, p_slA = 0, p_gB = 0, p_slB = 0, p_nA = 0;
+#ifdef ADX_STAMP
+    unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
-    for (int d = 4; d <= N; ++d) {
-        const int cur = d & 1;
-        const int db = d - 1;
+    for (int d = 4; d <= N + 2; ++d) {
+        STAMP(10);
+        const int buf = d & 1;
+        float *scr = L.scr + buf * NT;
+        const float *pscr = L.scr + (buf ^ 1) * NT;
+        float *scrC = L.scr + 2 * NT;
+        // ---------------- finalize items of the previous iteration
+        const int df = d - 1;                     // qb diagonal to finish
+        const int cdf = (df >= 4 && df <= N - 1) ? N - df : 0;
+        const int dq = d - 3;                     // qm diagonal to finish
+        const int cq = (dq >= 4 && dq <= N - 6) ? N - dq : 0;
+        const int jq = d - 2;                     // q5 index to finish
+        if (tid < cdf) {
+            const int i = tid + 1, j = i + df;
+            const int idx = off(df, N) + i - 1;
+            const int r = pinv(L, df & 3)[i];
+            const int si = L.S[i], sj = L.S[j];
+            const int sim = L.S[i - 1], sjp = L.S[j + 1];
+            const int btype = ptype(si, sj);
+            float qbv = 0.f;
+            if (r != 0xFF) {
+                const int ch = r / WAVE, ln = r % WAVE;
+                for (int sl = 0; sl < p_slA; sl++) qbv += pscr[(sl * p_gA + ch) * WAVE + ln];
+                const int u = df - 1;
+                if (L.up[i + 1] >= u) {
+                    float h = -1.f;
+                    if (u == 3 || u == 4 || u == 6) {
+                        const uint32_t key = hp_key(L.S, i, u + 2);
+                        for (int k = 0; k < nsp; k++)
+                            if (__float_as_uint(L.dt[DT_SPK + k]) == key) { h = L.dt[DT_SPV + k]; break; }
+                    }
+                    if (h < 0.f)
+                        h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + btype]
+                                                        : L.dt[DT_MMH + btype * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
+                    qbv += h;
+                }
+                if (df == mlen - 1 && L.mat[i]) qbv += mextra;
+            }
+            const int code = rtype(btype) * 25 + sjp * 5 + sim;
+            L.qbm[idx] = qbv * L.dt[DT_MMI + code];
+            L.cc[idx] = static_cast<uint8_t>(code);
+            if (df <= N - 6) {
+                float q1 = qbv * L.dt[DT_MLS + btype * 25 + sim * 5 + sjp];
+                if (df >= 5 && L.up[j] >= 1) q1 = fmaf(L.qm1[colb(j - 1) + i - 1], mlbase_sig, q1);
+                L.qm1[colb(j) + i - 1] = q1;
+            }
+        } else if (tid < cdf + cq) {
+            const int r = tid - cdf;
+            const int ch = r / WAVE, ln = r % WAVE;
+            float sq = 0.f;
+            for (int sl = 0; sl < p_slB; sl++) sq += pscr[(p_nA + sl * p_gB + ch) * WAVE + ln];
+            L.qm[rowb(r + 1, N) + dq - 4] = sq;
+        } else if (tid == cdf + cq && jq >= 4 && jq <= N) {
+            L.q5[jq] = ((L.up[jq] >= 1) ? L.q5[jq - 1] * sig1 : 0.f) + scrC[jq & 1];
+        }
+        if (wid == NW - 1 && d + 1 <= N - 1) build_plist(L, N, d + 1, (d + 1) & 3, lane);
+        STAMP(0);
+
+        // ---------------- jobs
         const bool jobA = d <= N - 1;
-        const bool jobB = db >= 4 && db <= N - 6;
-        const int cp = jobA ? L.pcount[cur] : 0;
+        const int dbq = d - 2;
+        const bool jobB = dbq >= 4 && dbq <= N - 6;
+        const int cp = jobA ? L.pcount[d & 3] : 0;
+        const int cb = jobB ? N - dbq : 0;
         const int gA = (cp + WAVE - 1) / WAVE;
-        const int slA = gA ? NW / gA : 0;
-        const int cb = jobB ? N - db : 0;
         const int gB = (cb + WAVE - 1) / WAVE;
-        const int slB = gB ? NW / gB : 0;
+        const int umax = d - 6 < 30 ? d - 6 : 30;
+        // job A term list per cell: [7 small shapes | generic (u = 6..umax, n1 = 2..u-2)
+        // | multiloop closing (tp = 6..d-5) | umax bulge pairs | umax-3 1xn pairs]
+        const int nGen = umax >= 6 ? ((umax - 3) * (umax - 2)) / 2 - 3 : 0;
+        const int nML = d > 10 ? d - 10 : 0;
+        const int nBul = umax > 0 ? umax : 0;
+        const int n1n = umax > 3 ? umax - 3 : 0;
+        const int nT = 7 + nGen + nML + nBul + n1n;
+        const int nB = jobB ? dbq - 3 : 0;
+        int nA = 0;
+        if (gA && gB) {
+            const int wA = gA * (6 + nGen + nML + 3 * (nBul + n1n));
+            const int wB = gB * 2 * nB;
+            nA = (NW * wA + (wA + wB) / 2) / (wA + wB);
+            if (nA < gA) nA = gA;
+            if (nA > NW - gB) nA = NW - gB;
+        } else if (gA) {
+            nA = NW;
+        }
+        const int slA = gA ? nA / gA : 0;
+        const int slB = gB ? (NW - nA) / gB : 0;
 
-        // ============================== phase A
-        if (cp > 0 && wid < gA * slA) {
+        if (wid < gA * slA) {
+            // ====================== job A: qb(d) partials
             const int ch = wid % gA, sl = wid / gA;
             const int r = ch * WAVE + lane;
             const bool active = r < cp;
-            const int i = plist(L, cur)[active ? r : 0];
+            const int i = plist(L, d & 3)[active ? r : 0];
             const int j = i + d;
-            const int si = L.S[i], sj = L.S[j];
-            const int type = ptype(si, sj);
+            const int type = ptype(L.S[i], L.S[j]);
             const int si1 = L.S[i + 1], sj1 = L.S[j - 1];
             const int A_ = L.up[i + 1], B_ = L.dn[j - 1];
-            const float mm1n_ij = T.mm1n[type][si1][sj1];
-            const float mm23_ij = T.mm23[type][si1][sj1];
-            const float tau_ij = T.termAU[type];
-            float accS = 0.f, accG = 0.f, accM = 0.f;
-            const int nInt = (d >= 6) ? X.ncnt[d - 6 < 30 ? d - 6 : 30] : 0;
-            int t = sl;
-            for (; t < nInt; t += slA) {
-                const TermDesc e = X.terms[t];
-                const int n1 = e.n1, n2 = e.n2;
-                const int base = off(d - 2 - e.u, N);
-                const int p = i + 1 + n1, q = j - 1 - n2;
-                const int idx = base + p - 1;
-                const bool ok = (n1 <= A_) && (n2 <= B_);
-                const float fo = ok ? e.f : 0.f;
-                if (e.kind == K_GENERIC) {
-                    float vq;
-                    if constexpr (QBM) {
-                        vq = L.qbm[idx];
-                    } else {
-                        const int t2 = RTYPE_D[ptype(L.S[p], L.S[q])];
-                        vq = L.qb[idx] * T.mmI[t2][L.S[q + 1]][L.S[p - 1]];
-                    }
-                    accG = fmaf(vq, fo, accG);
-                } else {
-                    const float vq = L.qb[idx];
-                    const int sp = L.S[p], sq = L.S[q];
-                    const int type2 = ptype(sq, sp);
-                    float fac;
-                    switch (e.kind) {
-                    case K_STACK:
-                    case K_BULGE1: fac = T.stack[type][type2]; break;
-                    case K_BULGE: fac = tau_ij * T.termAU[type2]; break;
-                    case K_I11: fac = T.int11[type][type2][si1][sj1]; break;
-                    case K_I21: fac = T.int21[type][type2][si1][L.S[q + 1]][sj1]; break;
-                    case K_I12: fac = T.int21[type2][type][L.S[q + 1]][si1][L.S[p - 1]]; break;
-                    case K_I22: fac = T.int22[type][type2][si1][L.S[p - 1]][L.S[q + 1]][sj1]; break;
-                    case K_I23: fac = mm23_ij * T.mm23[type2][L.S[q + 1]][L.S[p - 1]]; break;
-                    default: /* K_1N */ fac = mm1n_ij * T.mm1n[type2][L.S[q + 1]][L.S[p - 1]]; break;
-                    }
-                    accS = fmaf(vq * fac, fo, accS);
+            const int ocode = type * 25 + si1 * 5 + sj1;
+            const float mmI_ij = L.dt[DT_MMI + ocode];
+            const float mlc_ij = L.dt[DT_MLS + rtype(type) * 25 + sj1 * 5 + si1];
+            const bool free_cell = !active || (A_ >= umax && B_ >= umax);
+            const bool masked = constrained && (__ballot(!free_cell) != 0ull);
+            const int t0 = (sl * nT) / slA, t1 = ((sl + 1) * nT) / slA;
+            const float tau_ij = type > 2 ? eTAU : 1.f;
+            // ---- small shapes: int11/21/22 come from HBM/L2, so they are issued
+            // first and consumed after the LDS-bound loops
+            float smq[7], smf[7];
+#pragma unroll
+            for (int s = 0; s < 7; s++) {
+                smq[s] = 0.f;
+                smf[s] = 0.f;
+                const int n1 = (s == 0) ? 0 : (s == 1 || s == 2) ? 1 : (s == 6) ? 3 : 2;
+                const int n2 = (s == 0) ? 0 : (s == 1 || s == 3) ? 1 : (s == 2 || s == 4 || s == 6) ? 2 : 3;
+                const int u = n1 + n2;
+                if (s >= t0 && s < t1 && u <= umax) {
+                    const int ix = off(d - 2 - u, N) + i + n1;
+                    const int code = L.cc[ix];
+                    const int t2 = (code * 41) >> 10;
+                    const int p = i + 1 + n1, q = j - 1 - n2;
+                    const int sp1 = L.S[p - 1], sq1 = L.S[q + 1];
+                    const bool ok = !masked || ((n1 <= A_) & (n2 <= B_));
+                    smq[s] = ok ? L.qbm[ix] * ct[CT_INVMM + code] : 0.f;
+                    if (s == 0) smf[s] = ct[CT_STK + type * 8 + t2] * ct[CT_FSM + 0];
+                    else if (s == 1) smf[s] = T.int11[type][t2][si1][sj1] * ct[CT_FSM + 2];
+                    else if (s == 2) smf[s] = T.int21[type][t2][si1][sq1][sj1] * ct[CT_FSM + 3];
+                    else if (s == 3) smf[s] = T.int21[t2][type][sq1][si1][sp1] * ct[CT_FSM + 3];
+                    else if (s == 4) smf[s] = T.int22[type][t2][si1][sp1][sq1][sj1] * ct[CT_FSM + 4];
+                    else smf[s] = ct[CT_M23O + ocode] * ct[CT_M23O + code] * ct[CT_FSM + 5];
                 }
             }
-            // multiloop closed by (i,j): k = i + tp, tp in [6, d-5]
-            const int nML = d - 10;
-            for (int m = t - nInt; m < nML; m += slA) {
-                const int tp = m + 6;
-                const int idx1 = off(tp - 2, N) + i;           // (i+1, i+tp-1)
-                const int idx2 = off(d - 1 - tp, N) + i + tp - 1;  // (i+tp, j-1)
-                accM = fmaf(L.qm[idx1], L.qm1[idx2], accM);
+            STAMP(1);
+            float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#ifndef ADX_ABL_GENERIC
+            // ---- generic interior loops: contiguous n1 runs of one u per row
+            {
+                const int gs = (t0 > 7 ? t0 : 7) - 7, ge = (t1 < 7 + nGen ? t1 : 7 + nGen) - 7;
+                if (gs < ge) {
+                    int u = 6, rs = 0;
+                    while (rs + (u - 3) <= gs) { rs += u - 3; u++; }
+                    int idx = gs;
+                    while (idx < ge) {
+                        const int a = 2 + (idx - rs);
+                        const int rowend = rs + (u - 3);
+                        const int e = (ge < rowend ? ge : rowend) - rs + 2;  // n1 in [a, e)
+                        const float *fr = XS->fgen + (u - 6) * FG_ROW - 2;    // fr[n1] (scalar loads)
+                        const float *q = L.qbm + off(d - 2 - u, N) + i;  // q[n1] = qbm(i+1+n1, j-1-u+n1)
+                        int n1 = a;
+                        if (!masked) {
+                            for (; n1 + 8 <= e; n1 += 8) {
+                                float qv[8], fv[8];
+#pragma unroll
+                                for (int k = 0; k < 8; k++) { qv[k] = q[n1 + k]; fv[k] = fr[n1 + k]; }
+#pragma unroll
+                                for (int k = 0; k < 8; k++) g[k] = fmaf(qv[k], fv[k], g[k]);
+                            }
+                            for (; n1 + 2 <= e; n1 += 2) {
+                                const float q0 = q[n1], q1 = q[n1 + 1];
+                                g[0] = fmaf(q0, fr[n1], g[0]);
+                                g[1] = fmaf(q1, fr[n1 + 1], g[1]);
+                            }
+                            if (n1 < e) g[2] = fmaf(q[n1], fr[n1], g[2]);
+                        } else {
+                            const int lo = u - B_;  // n2 <= B_  <=>  n1 >= u - B_
+                            for (; n1 + 4 <= e; n1 += 4) {
+                                float qv[4];
+#pragma unroll
+                                for (int k = 0; k < 4; k++) qv[k] = q[n1 + k];
+#pragma unroll
+                                for (int k = 0; k < 4; k++) {
+                                    const bool ok = (n1 + k <= A_) & (n1 + k >= lo);
+                                    g[k] = fmaf(qv[k], ok ? fr[n1 + k] : 0.f, g[k]);
+                                }
+                            }
+                            for (; n1 < e; n1++) {
+                                const bool ok = (n1 <= A_) & (n1 >= lo);
+                                g[4] = fmaf(q[n1], ok ? fr[n1] : 0.f, g[4]);
+                            }
+                        }
+                        idx = rs + (e - 2);
+                        rs = rowend;
+                        u++;
+                    }
+                }
             }
-            const float mmI_ij = T.mmI[type][si1][sj1];
-            const float mlc_ij = X.mlclosing * T.mlstem[RTYPE_D[type]][sj1][si1];
-            float part = accS + accG * mmI_ij + accM * mlc_ij;
-            L.scrA[(sl * gA + ch) * WAVE + lane] = part;
-        }
-        if (cb > 0 && wid < gB * slB) {
-            const int ch = wid % gB, sl = wid / gB;
+#endif
+            STAMP(2);
+            float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#ifndef ADX_ABL_ML
+            // ---- multiloop closed by (i,j): qm[i+1][k-1] * qm1[k][j-1], k = i + tp
+            {
+                const int b0 = 7 + nGen;
+                const int ms = (t0 > b0 ? t0 : b0) - b0, me = (t1 < b0 + nML ? t1 : b0 + nML) - b0;
+                if (ms < me) {
+                    const float *qa = L.qm + rowb(i + 1, N);          // qa[m] = qm[i+1][i+tp-1], tp = 6 + m
+                    const float *qb1 = L.qm1 + colb(j - 1) + i + 5;   // qb1[m] = qm1[i+tp][j-1]
+                    int mm = ms;
+                    for (; mm + 8 <= me; mm += 8) {
+                        float av[8], bv[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) { av[k] = qa[mm + k]; bv[k] = qb1[mm + k]; }
+#pragma unroll
+                        for (int k = 0; k < 8; k++) m[k] = fmaf(av[k], bv[k], m[k]);
+                    }
+                    for (; mm < me; mm++) m[0] = fmaf(qa[mm], qb1[mm], m[0]);
+                }
+            }
+#endif
+            STAMP(3);
+            float sA = 0.f, sB = 0.f, sC = 0.f, sD = 0.f;
+#ifndef ADX_ABL_SPECIAL
+            {
+                const int b0 = 7 + nGen + nML;
+                // bulges (0,n) and (n,0), n = 1..umax: unit n - 1 covers both sides
+                {
+                    const int bs = (t0 > b0 ? t0 : b0) - b0;
+                    const int be = (t1 < b0 + nBul ? t1 : b0 + nBul) - b0;
+                    int n = bs + 1;
+                    int o = off(d - 2 - n, N) + i;  // cell (i+1, j-1-n)
+                    if (n == 1 && n <= be) {
+                        const int c0 = L.cc[o], c1 = L.cc[o + 1];
+                        const float v0 = L.qbm[o], v1 = L.qbm[o + 1];
+                        const float f0 = ct[CT_FSM + 1];
+                        const float x0 = ct[CT_INVMM + c0] * ct[CT_STK + type * 8 + ((c0 * 41) >> 10)] * f0;
+                        const float x1 = ct[CT_INVMM + c1] * ct[CT_STK + type * 8 + ((c1 * 41) >> 10)] * f0;
+                        const bool ok0 = !masked || (1 <= B_), ok1 = !masked || (1 <= A_);
+                        sA = fmaf(v0, ok0 ? x0 : 0.f, sA);
+                        sB = fmaf(v1, ok1 ? x1 : 0.f, sB);
+                        o -= N - (d - 4);  // off(D-1) = off(D) - (N - D + 1), D = d-3
+                        n++;
+                    }
+                    // two units per iteration: 4 independent cc/qbm loads in flight
+                    for (; n + 1 <= be; n += 2) {
+                        const int o2 = o - (N - (d - 3 - n));
+                        const int c0 = L.cc[o], c1 = L.cc[o + n], c2 = L.cc[o2], c3 = L.cc[o2 + n + 1];
+                        const float v0 = L.qbm[o], v1 = L.qbm[o + n], v2 = L.qbm[o2], v3 = L.qbm[o2 + n + 1];
+                        const float fb0 = XS->ctab[CT_FB + n] * tau_ij, fb1 = XS->ctab[CT_FB + n + 1] * tau_ij;
+                        const float x0 = ct[CT_BUL + c0] * fb0, x1 = ct[CT_BUL + c1] * fb0;
+                        const float x2 = ct[CT_BUL + c2] * fb1, x3 = ct[CT_BUL + c3] * fb1;
+                        const bool ok0 = !masked || (n <= B_), ok1 = !masked || (n <= A_);
+                        const bool ok2 = !masked || (n + 1 <= B_), ok3 = !masked || (n + 1 <= A_);
+                        sA = fmaf(v0, ok0 ? x0 : 0.f, sA);
+                        sB = fmaf(v1, ok1 ? x1 : 0.f, sB);
+                        sC = fmaf(v2, ok2 ? x2 : 0.f, sC);
+                        sD = fmaf(v3, ok3 ? x3 : 0.f, sD);
+                        o = o2 - (N - (d - 4 - n));
+                    }
+                    if (n <= be) {
+                        const int c0 = L.cc[o], c1 = L.cc[o + n];
+                        const float fb = ct[CT_FB + n] * tau_ij;
+                        const bool ok0 = !masked || (n <= B_), ok1 = !masked || (n <= A_);
+                        sA = fmaf(L.qbm[o], ok0 ? ct[CT_BUL + c0] * fb : 0.f, sA);
+                        sB = fmaf(L.qbm[o + n], ok1 ? ct[CT_BUL + c1] * fb : 0.f, sB);
+                    }
+                }
+                // 1 x nl and nl x 1, nl = 3..umax-1: unit nl - 3 covers both sides
+                {
+                    const int s0 = b0 + nBul;
+                    const int bs = (t0 > s0 ? t0 : s0) - s0, be = t1 - s0;
+                    if (bs < be) {
+                        const float mo = ct[CT_ONEN + ocode] * mmI_ij;  // outer mismatch_1n
+                        int nl = bs + 3;
+                        const int nle = be + 3;
+                        int o = off(d - 3 - nl, N) + i;  // cell (i+2, j-1-nl) at o + 1
+                        for (; nl + 1 < nle; nl += 2) {
+                            const int o2 = o - (N - (d - 4 - nl));
+                            const int c0 = L.cc[o + 1], c1 = L.cc[o + nl], c2 = L.cc[o2 + 1], c3 = L.cc[o2 + nl + 1];
+                            const float v0 = L.qbm[o + 1], v1 = L.qbm[o + nl];
+                            const float v2 = L.qbm[o2 + 1], v3 = L.qbm[o2 + nl + 1];
+                            const float f0 = XS->ctab[CT_F1N + nl] * mo, f1 = XS->ctab[CT_F1N + nl + 1] * mo;
+                            const bool ok0 = !masked || ((1 <= A_) & (nl <= B_));
+                            const bool ok1 = !masked || ((nl <= A_) & (1 <= B_));
+                            const bool ok2 = !masked || ((1 <= A_) & (nl + 1 <= B_));
+                            const bool ok3 = !masked || ((nl + 1 <= A_) & (1 <= B_));
+                            sA = fmaf(v0, ok0 ? ct[CT_ONEN + c0] * f0 : 0.f, sA);
+                            sB = fmaf(v1, ok1 ? ct[CT_ONEN + c1] * f0 : 0.f, sB);
+                            sC = fmaf(v2, ok2 ? ct[CT_ONEN + c2] * f1 : 0.f, sC);
+                            sD = fmaf(v3, ok3 ? ct[CT_ONEN + c3] * f1 : 0.f, sD);
+                            o = o2 - (N - (d - 5 - nl));
+                        }
+                        if (nl < nle) {
+                            const int c0 = L.cc[o + 1], c1 = L.cc[o + nl];
+                            const float f0 = ct[CT_F1N + nl] * mo;
+                            const bool ok0 = !masked || ((1 <= A_) & (nl <= B_));
+                            const bool ok1 = !masked || ((nl <= A_) & (1 <= B_));
+                            sA = fmaf(L.qbm[o + 1], ok0 ? ct[CT_ONEN + c0] * f0 : 0.f, sA);
+                            sB = fmaf(L.qbm[o + nl], ok1 ? ct[CT_ONEN + c1] * f0 : 0.f, sB);
+                        }
+                    }
+                }
+            }
+#endif
+            float sm = 0.f;
+#pragma unroll
+            for (int s = 0; s < 7; s++) sm = fmaf(smq[s], smf[s], sm);
+            const float gsum = ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
+            const float msum = ((m[0] + m[1]) + (m[2] + m[3])) + ((m[4] + m[5]) + (m[6] + m[7]));
+            const float part = ((sA + sB) + (sC + sD)) + sm + gsum * mmI_ij + msum * (mlclosing * mlc_ij);
+            scr[wid * WAVE + lane] = part;
+            STAMP(4);
+        } else if (wid >= nA && wid < nA + gB * slB) {
+            // ====================== job B: qm(dbq) partials
+            // qm[i][jb] = sum_t (pre(t) + qm[i][i+t-1]) * qm1[i+t][jb]
+            const int lw = wid - nA;
+            const int ch = lw % gB, sl = lw / gB;
             const int r = ch * WAVE + lane;
             const bool active = r < cb;
             const int i = (active ? r : 0) + 1;
+            const int jb = i + dbq;
             const int upi = L.up[i];
-            float acc = 0.f;
-            int t = sl;
-            const int tmax = db - 4;
-            for (; t <= tmax && t < 5; t += slB) {
-                const float q1 = L.qm1[off(db - t, N) + i + t - 1];
-                const float pre = (t <= upi) ? X.pwml[t] : 0.f;
-                acc = fmaf(pre, q1, acc);
+            const int t0 = (sl * nB) / slB, t1 = ((sl + 1) * nB) / slB;
+            const float *q1 = L.qm1 + colb(jb) + i - 1;   // q1[t] = qm1[i+t][jb]
+            const float *qr = L.qm + rowb(i, N) - 5;      // qr[t] = qm[i][i+t-1], t >= 5
+            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            int t = t0;
+            for (; t < t1 && t < 5; t++) a[0] = fmaf((t <= upi) ? XS->pwml[t] : 0.f, q1[t], a[0]);
+            if (!constrained) {
+                for (; t + 8 <= t1; t += 8) {
+                    float pv[8], rv[8], qv[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) { pv[k] = XS->pwml[t + k]; rv[k] = qr[t + k]; qv[k] = q1[t + k]; }
+#pragma unroll
+                    for (int k = 0; k < 8; k++) a[k] = fmaf(pv[k] + rv[k], qv[k], a[k]);
+                }
             }
-            for (; t <= tmax; t += slB) {
-                const float q1 = L.qm1[off(db - t, N) + i + t - 1];
-                const float pre = ((t <= upi) ? X.pwml[t] : 0.f) + L.qm[off(t - 1, N) + i - 1];
-                acc = fmaf(pre, q1, acc);
-            }
-            L.scrB[(sl * gB + ch) * WAVE + lane] = acc;
+            for (; t < t1; t++) a[1] = fmaf(((t <= upi) ? XS->pwml[t] : 0.f) + qr[t], q1[t], a[1]);
+            scr[wid * WAVE + lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+            STAMP(5);
         }
-        if (wid == NW - 1) {
-            // q5[j], j = d: sum_k q5[k-1] qb[k][j] ext(k,j)
-            const int j = d;
+        if (wid == NW - 1 && d - 1 >= 4 && d - 1 <= N) {
+            // ====================== job C: q5[j] partial, j = d-1
+            const int j = d - 1;
+            float extf[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int k = 1 + lane + c * WAVE;
+                extf[c] = 0.f;
+                if (k <= j - 4) {
+                    const int type = ptype(L.S[k], L.S[j]);
+                    extf[c] = L.dt[DT_EXT + type * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + ((j < N) ? L.S[j + 1] : 5)];
+                }
+            }
             float acc = 0.f;
-            for (int k = 1 + lane; k <= j - 4; k += WAVE) {
-                const float vq = L.qb[off(j - k, N) + k - 1];
-                const int type = ptype(L.S[k], L.S[j]);
-                const int c5 = (k > 1) ? L.S[k - 1] : 5;
-                const int c3 = (j < N) ? L.S[j + 1] : 5;
-                acc = fmaf(L.q5[k - 1] * vq, T.ext[type][c5][c3], acc);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int k = 1 + lane + c * WAVE;
+                if (k <= j - 4) {
+                    const int ix = off(j - k, N) + k - 1;
+                    acc = fmaf(L.q5[k - 1] * L.qbm[ix], ct[CT_INVMM + L.cc[ix]] * extf[c], acc);
+                }
             }
             acc = wave_sum(acc);
-            if (lane == 0) L.misc[0] = acc;
+            if (lane == 0) scrC[j & 1] = acc;
+            STAMP(6);
         }
+        p_gA = gA;
+        p_slA = slA;
+        p_gB = gB;
+        p_slB = slB;
+        p_nA = nA;
+        STAMP(8);
         __syncthreads();
-
-        // ============================== phase B
-        const int cd = jobA ? N - d : 0;
-        const int nitems = cd + cb + 1;
-        for (int w = tid; w < nitems; w += NT) {
-            if (w < cd) {
-                const int i = w + 1, j = i + d;
-                const int idx = off(d, N) + i - 1;
-                const int r = pinv(L, cur)[i];
-                const int si = L.S[i], sj = L.S[j];
-                const int type = ptype(si, sj);
-                float qbv = 0.f;
-                if (r != 0xFF) {
-                    const int ch = r / WAVE, ln = r % WAVE;
-                    for (int sl = 0; sl < slA; sl++) qbv += L.scrA[(sl * gA + ch) * WAVE + ln];
-                    const int u = d - 1;
-                    if (L.up[i + 1] >= u) {
-                        float hpv = -1.f;
-                        if (u == 3 || u == 4 || u == 6) {
-                            const uint32_t key = hp_key(L.S, i, u + 2);
-                            for (int k = 0; k < X.n_special; k++)
-                                if (X.sp_key[k] == key) { hpv = X.sp_val[k]; break; }
-                        }
-                        if (hpv < 0.f)
-                            hpv = X.hp[u] * ((u == 3) ? T.termAU[type] : T.mmH[type][L.S[i + 1]][L.S[j - 1]]);
-                        qbv += hpv;
-                    }
-                    if (L.mat[i] && d == X.motif_len - 1) qbv += X.motif_extra;
-                }
-                L.qb[idx] = qbv;
-                if constexpr (QBM) {
-                    L.qbm[idx] = qbv * T.mmI[RTYPE_D[type]][L.S[j + 1]][L.S[i - 1]];
-                }
-                if (d <= N - 6) {
-                    float q1 = qbv * T.mlstem[type][L.S[i - 1]][L.S[j + 1]];
-                    if (d >= 5 && L.up[j] >= 1) q1 = fmaf(L.qm1[off(d - 1, N) + i - 1], mlbase_sig, q1);
-                    L.qm1[idx] = q1;
-                }
-            } else if (w < cd + cb) {
-                const int r = w - cd;
-                const int i = r + 1;
-                const int ch = r / WAVE, ln = r % WAVE;
-                float s = 0.f;
-                for (int sl = 0; sl < slB; sl++) s += L.scrB[(sl * gB + ch) * WAVE + ln];
-                L.qm[off(db, N) + i - 1] = s;
-            } else {
-                L.q5[d] = ((L.up[d] >= 1) ? L.q5[d - 1] * sig1 : 0.f) + L.misc[0];
-            }
-        }
-        if (wid == 0 && d + 1 <= N - 1) build_plist(L, N, d + 1, cur ^ 1, lane);
-        __syncthreads();
+        STAMP(9);
     }
+#ifdef ADX_STAMP
+    if (lane == 0 && wid < 16)
+        for (int k = 0; k < 12; k++) atomicAdd(&g_stamps[wid][k], st_acc[k]);
+#endif
     const float z = L.q5[N];
     const double lnZ = log(static_cast<double>(z)) - N * X.log_sigma;
     return -X.kT * lnZ;
@@ -416,11 +704,12 @@ __device__ double combine_score(const KArgs &ka, const Lds &L, double *terms_out
     return score;
 }
 
-template <int NT, bool QBM>
-__device__ double score_sequence(const KArgs &ka, const uint8_t *raw, const Lds &L,
+template <int NT>
+__device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
+                                 const uint8_t *raw, const Lds &L,
                                  float *dG_out, double *terms_out) {
     for (int v = 0; v < ka.n_variants; v++) {
-        const double g = pf_inside<NT, QBM>(ka, v, raw, L);
+        const double g = pf_inside<NT>(ka, v, raw, L, XS);
         if (threadIdx.x == 0) {
             L.G[v] = g;
             if (dG_out) dG_out[v] = static_cast<float>(g);
@@ -432,17 +721,20 @@ __device__ double score_sequence(const KArgs &ka, const uint8_t *raw, const Lds 
     return s;
 }
 
-template <int NT, bool QBM>
+template <int NT>
 __global__ void __launch_bounds__(NT, 4)
-score_kernel(KArgs ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG) {
+score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
+             double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Lds L = carve<NT>(smem, ka, QBM);
+    const Lds L = carve<NT>(smem, ka);
     const int w = blockIdx.x;
     if (w >= W) return;
+    if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
+    load_ctab<NT>(ka, L);
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
-    const double s = score_sequence<NT, QBM>(ka, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
+    const double s = score_sequence<NT>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
                                              terms ? terms + size_t(w) * nt : nullptr);
     if (threadIdx.x == 0) scores[w] = s;
 }
@@ -512,235 +804,202 @@ __device__ double mt_canonical(MtView &g, int lane) {
 }
 
 // ---------------------------------------------------------------- MC step
-// One workgroup = one walker; the walker state that must survive the fold
-// (scores, thermostat state, counters) is kept in LDS, not in registers, so
-// the PF loop has the whole register file.
-template <int NT, bool QBM>
-__global__ void __launch_bounds__(NT, 4) step_kernel(KArgs ka, StepArgs st) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Lds L = carve<NT>(smem, ka, QBM);
+// One MonteCarlo::apply iteration (sampling.cc:55-99) = three launches on one
+// stream: propose_kernel (thermostat, RNG streams, mutation move, unchanged
+// check; one wave per walker) -> score_kernel masked to the walkers whose
+// sequence changed -> accept_kernel (Metropolis, one thread per walker).
+// Splitting keeps the fold kernel's register allocation free of the MC state.
+__global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step, int s) {
     const int w = blockIdx.x;
+    const int lane = threadIdx.x;
     if (w >= st.W) return;
-    const int tid = threadIdx.x, lane = tid & (WAVE - 1);
-    const int wid = uni(tid / WAVE);
-    const int Nraw = ka.Nraw;
-    const int nt_tot = ka.n_terms * ka.n_ctx_eff;
-    uint8_t *cur = st.cur_seq + size_t(w) * Nraw;
+    if (st.err[w]) {
+        if (lane == 0) st.changed[w] = 0;
+        return;
+    }
+    __shared__ uint32_t mt[2 * MT_WORDS];
+    uint8_t *cur = st.cur_seq + size_t(w) * st.Nraw;
     uint32_t *gA = st.mtA + size_t(w) * MT_WORDS;
     uint32_t *gC = st.mtC + size_t(w) * MT_WORDS;
-    // LDS-resident walker state
-    double *sd = L.dscr;                                  // 0 current 1 last_diff 2 autoT 3 u 4 prop 5 median
-    int *mi = reinterpret_cast<int *>(L.misc + 4);        // 0 pick 1 base 2 err 3 changed 4 ntrain 5 werr 6..9 counts
-    if (tid == 0) {
-        sd[0] = st.cur_score[w];
-        sd[1] = st.last_diff[w];
-        sd[2] = st.auto_T[w];
-        mi[4] = st.ntrain[w];
-        mi[5] = st.err[w];
-        mi[6] = mi[7] = mi[8] = mi[9] = 0;
-    }
-    __syncthreads();
-
-    for (int s = 0; s < st.nsteps; s++) {
-        if (mi[5] != 0) break;
-        const long long step = st.step0 + s;
-        // ---- thermostat (sampling.cc:59; 309-401)
-        double T;
-        if (st.thermo_kind == 0) {
-            T = st.t_fixed;
-        } else if (st.thermo_kind == 1) {
-            const int Nc = st.cycle_len;
-            T = ((st.t_lo - st.t_hi) / Nc) * double(int(step % Nc)) + st.t_hi;
-        } else {
-            double *tr = st.train + size_t(w) * st.period;
-            const int nt0 = mi[4];
-            __syncthreads();
-            if (tid == 0) {
-                tr[nt0] = sd[1];
-                mi[4] = nt0 + 1;
-            }
-            __syncthreads();
-            if (nt0 + 1 >= st.period) {
-                // nth_element(n/2): a value whose rank window covers n/2
-                const int n = nt0 + 1, k = n / 2;
-                if (wid == 0) {
-                    double found = 0.0;
-                    bool have = false;
-                    for (int e = lane; e < n; e += WAVE) {
-                        const double x = tr[e];
-                        int less = 0, eq = 0;
-                        for (int f = 0; f < n; f++) {
-                            const double y = tr[f];
-                            less += (y < x);
-                            eq += (y == x);
-                        }
-                        if (less <= k && k < less + eq) { found = x; have = true; }
-                    }
-                    const unsigned long long m = __ballot(have);
-                    const int src = m ? __ffsll((long long)m) - 1 : 0;
-                    const double med = __shfl(found, src, WAVE);
-                    if (lane == 0) {
-                        const double t = med / log(st.target_rate);
-                        sd[2] = t > 0.0 ? t : 0.0;
-                        mi[4] = 0;
-                    }
+    // ---- thermostat (sampling.cc:59; 309-401)
+    double T;
+    if (st.thermo_kind == 0) {
+        T = st.t_fixed;
+    } else if (st.thermo_kind == 1) {
+        const int Nc = st.cycle_len;
+        T = ((st.t_lo - st.t_hi) / Nc) * double(int(step % Nc)) + st.t_hi;
+    } else {
+        double *tr = st.train + size_t(w) * st.period;
+        const int n = st.ntrain[w] + 1;
+        if (lane == 0) tr[n - 1] = st.last_diff[w];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        T = st.auto_T[w];
+        if (n >= st.period) {
+            // nth_element(n/2): a value whose rank window covers n/2
+            const int k = n / 2;
+            double found = 0.0;
+            bool have = false;
+            for (int e = lane; e < n; e += WAVE) {
+                const double x = tr[e];
+                int less = 0, eq = 0;
+                for (int f = 0; f < n; f++) {
+                    const double y = tr[f];
+                    less += (y < x);
+                    eq += (y == x);
                 }
-                __syncthreads();
+                if (less <= k && k < less + eq) { found = x; have = true; }
             }
-            T = sd[2];
-        }
-
-        // ---- move: wave 0 draws from stream A (and C if the step is scored)
-        if (wid == 0) {
-            uint32_t *mA = L.rng, *mC = L.rng + MT_WORDS;
-            for (int k = lane; k < 624; k += WAVE) {
-                mA[k] = gA[k];
-                mC[k] = gC[k];
-            }
-            MtView a{mA, int(gA[624]), false}, c{mC, int(gC[624]), false};
-            const int pick = int(mt_uniform(a, uint32_t(st.M), lane));
-            const int bcode = int(mt_uniform(a, 4u, lane)) + 1;  // "ACGU"[r]
-            const int e = st.clo_err[pick];
-            bool changed = false;
-            if (e == 0) {
-                for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE) {
-                    const int pos = st.clo_pos[k];
-                    const int nb = st.clo_par[k] ? 5 - bcode : bcode;
-                    if (cur[pos] != nb) changed = true;
-                }
-                changed = __ballot(changed) != 0ull;
-            }
-            double u = 0.0;
-            if (e == 0 && changed) u = mt_canonical(c, lane);
-            for (int k = lane; k < 624; k += WAVE) {
-                if (a.twisted) gA[k] = mA[k];
-                if (c.twisted) gC[k] = mC[k];
-            }
+            const unsigned long long m = __ballot(have);
+            const int src = m ? __ffsll((long long)m) - 1 : 0;
+            const double med = __shfl(found, src, WAVE);
+            const double t = med / log(st.target_rate);
+            T = t > 0.0 ? t : 0.0;
             if (lane == 0) {
-                gA[624] = uint32_t(a.idx);
-                gC[624] = uint32_t(c.idx);
-                mi[0] = pick;
-                mi[1] = bcode;
-                mi[2] = e;
-                mi[3] = changed ? 1 : 0;
-                sd[3] = u;
+                st.auto_T[w] = T;
+                st.ntrain[w] = 0;
             }
+        } else if (lane == 0) {
+            st.ntrain[w] = n;
         }
-        __syncthreads();
-        if (mi[2] != 0) {
-            if (tid == 0) mi[5] = mi[2];
-            break;
-        }
-        const bool changed = mi[3] != 0;
-        double *tv = (st.tr_terms) ? st.tr_terms + (size_t(s) * st.W + w) * nt_tot : nullptr;
-        if (changed) {
-            const int pick = mi[0], bcode = mi[1];
-            for (int k = tid; k < Nraw; k += NT) L.raw[k] = cur[k];
-            __syncthreads();
-            for (int k = st.clo_off[pick] + tid; k < st.clo_off[pick + 1]; k += NT) {
-                const int pos = st.clo_pos[k];
-                L.raw[pos] = uint8_t(st.clo_par[k] ? 5 - bcode : bcode);
-            }
-            __syncthreads();
-            const double sc = score_sequence<NT, QBM>(ka, L.raw, L, nullptr, tv);
-            if (tid == 0) {
-                const double diff = sc - sd[0];
-                sd[1] = diff;
-                sd[4] = sc;
-                const double crit = exp(diff / T);
-                int outcome;
-                if (crit < sd[3]) {
-                    outcome = 0;
-                } else {
-                    outcome = (diff > 0) ? 3 : 1;
-                    sd[0] = sc;
-                }
-                mi[3] = 2 + outcome;  // 2 REJECT, 3 WORSENED, 5 IMPROVED
-            }
-            __syncthreads();
-            if (mi[3] != 2)
-                for (int k = tid; k < Nraw; k += NT) cur[k] = L.raw[k];
-        } else if (tv && tid == 0) {
-            for (int k = 0; k < nt_tot; k++) tv[k] = __builtin_nan("");
-        }
-        if (tid == 0) {
-            const int outcome = changed ? mi[3] - 2 : 2;
-            mi[6 + outcome]++;
-            if (st.tr_pos) {
-                const size_t r = size_t(s) * st.W + w;
-                st.tr_pos[r] = st.mut[mi[0]];
-                st.tr_base[r] = int8_t(mi[1]);
-                st.tr_outcome[r] = outcome;
-                st.tr_temp[r] = T;
-                st.tr_prop[r] = changed ? sd[4] : __builtin_nan("");
-                st.tr_cur[r] = sd[0];
-                st.tr_u[r] = changed ? sd[3] : __builtin_nan("");
-            }
-        }
-        __syncthreads();
+    }
+    // ---- move: stream A (and C if the step will be scored)
+    uint32_t *mA = mt, *mC = mt + MT_WORDS;
+    for (int k = lane; k < 624; k += WAVE) {
+        mA[k] = gA[k];
+        mC[k] = gC[k];
     }
     __syncthreads();
-    if (tid == 0) {
-        for (int k = 0; k < 4; k++) st.counters[size_t(w) * 4 + k] += mi[6 + k];
-        st.cur_score[w] = sd[0];
-        st.last_diff[w] = sd[1];
-        st.auto_T[w] = sd[2];
-        st.ntrain[w] = mi[4];
-        st.err[w] = mi[5];
+    MtView a{mA, int(gA[624]), false}, c{mC, int(gC[624]), false};
+    const int pick = int(mt_uniform(a, uint32_t(st.M), lane));
+    const int bcode = int(mt_uniform(a, 4u, lane)) + 1;  // "ACGU"[r]
+    const int e = st.clo_err[pick];
+    bool changed = false;
+    if (e == 0) {
+        for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE) {
+            const int pos = st.clo_pos[k];
+            const int nb = st.clo_par[k] ? 5 - bcode : bcode;
+            if (cur[pos] != nb) changed = true;
+        }
+        changed = __ballot(changed) != 0ull;
+    }
+    double u = 0.0;
+    if (e == 0 && changed) u = mt_canonical(c, lane);
+    for (int k = lane; k < 624; k += WAVE) {
+        if (a.twisted) gA[k] = mA[k];
+        if (c.twisted) gC[k] = mC[k];
+    }
+    if (changed) {
+        uint8_t *prop = st.prop_seq + size_t(w) * st.Nraw;
+        for (int k = lane; k < st.Nraw; k += WAVE) prop[k] = cur[k];
+        __syncthreads();
+        for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE)
+            prop[st.clo_pos[k]] = uint8_t(st.clo_par[k] ? 5 - bcode : bcode);
+    }
+    if (lane == 0) {
+        gA[624] = uint32_t(a.idx);
+        gC[624] = uint32_t(c.idx);
+        st.pick[w] = pick;
+        st.bcode[w] = bcode;
+        st.temp[w] = T;
+        st.u[w] = u;
+        st.changed[w] = (e != 0) ? 0 : (changed ? 1 : 0);
+        if (e != 0) st.err[w] = e;
+        if (st.tr_pos) {
+            const size_t r = size_t(s) * st.W + w;
+            st.tr_pos[r] = st.mut[pick];
+            st.tr_base[r] = int8_t(bcode);
+            st.tr_temp[r] = T;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= st.W || st.err[w]) return;
+    const bool changed = st.changed[w] == 1;
+    int outcome = 2;  // ACCEPT_UNCHANGED
+    const double prop = st.prop_score[w];
+    if (changed) {
+        const double diff = prop - st.cur_score[w];
+        st.last_diff[w] = diff;
+        const double crit = exp(diff / st.temp[w]);
+        if (crit < st.u[w]) {
+            outcome = 0;
+        } else {
+            outcome = (diff > 0) ? 3 : 1;
+            st.cur_score[w] = prop;
+            const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
+            uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
+            for (int k = 0; k < st.Nraw; k++) c[k] = p[k];
+        }
+    }
+    st.counters[size_t(w) * 4 + outcome] += 1;
+    if (st.tr_pos) {
+        const size_t r = size_t(s) * st.W + w;
+        st.tr_outcome[r] = outcome;
+        st.tr_prop[r] = changed ? prop : __builtin_nan("");
+        st.tr_cur[r] = st.cur_score[w];
+        st.tr_u[r] = changed ? st.u[w] : __builtin_nan("");
+        if (!changed && st.tr_terms)
+            for (int k = 0; k < nt_tot; k++) st.tr_terms[r * nt_tot + k] = __builtin_nan("");
     }
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------- host launchers
-size_t lds_bytes(const KArgs &ka, bool qbm, int nt) {
+size_t lds_bytes(const KArgs &ka, bool /*unused*/, int nt) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     const size_t C = size_t(ka.cells);
-    size_t tb = C * 4 * (qbm ? 4 : 3);
-    if (tb < 2 * MT_WORDS * 4) tb = 2 * MT_WORDS * 4;
     const size_t NP = size_t(ka.Nmax) + 2;
-    size_t s = al(tb) + 2 * al(nt * 4) + al(NP * 4) + al(16 * 4) + al(MAX_VARIANTS * 8) +
-               al(16 * 8) + al(16) + 12 * al(NP);
-    return s;
+    return 3 * al(C * 4) + al(C) + al(2 * nt * 4 + 16) + al(CT_SIZE * 4) + al(size_t(896 + 2 * MAX_SPECIAL_HP + ka.Nmax + 1) * 4) + al(NP * 4) + al(16 * 4) +
+           al(size_t(ka.n_variants) * 8) + al(16) + 8 * al(NP) + al(8 * NP);
 }
 
 constexpr int NT_DEFAULT = 512;
 
-hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
-                        double *terms, float *dG, hipStream_t stream) {
-    const size_t lds = lds_bytes(ka, qbm, NT_DEFAULT);
-    if (qbm) {
-        auto k = score_kernel<NT_DEFAULT, true>;
+hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
+                          float *dG, const int *mask, hipStream_t stream) {
+    const size_t lds = lds_bytes(ka, true, NT_DEFAULT);
+    auto k = score_kernel<NT_DEFAULT>;
+    static size_t configured = 0;
+    if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(W), dim3(NT_DEFAULT), lds, stream, ka, seqs, W, scores, terms, dG);
-    } else {
-        auto k = score_kernel<NT_DEFAULT, false>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(W), dim3(NT_DEFAULT), lds, stream, ka, seqs, W, scores, terms, dG);
+        configured = lds;
     }
+    hipLaunchKernelGGL(k, dim3(W), dim3(NT_DEFAULT), lds, stream, ka, ka.X, seqs, W, scores, terms, dG, mask);
     return hipGetLastError();
 }
 
-hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream) {
-    const size_t lds = lds_bytes(ka, qbm, NT_DEFAULT);
-    if (qbm) {
-        auto k = step_kernel<NT_DEFAULT, true>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, double *scores,
+                        double *terms, float *dG, hipStream_t stream) {
+    return launch_score_m(ka, seqs, W, scores, terms, dG, nullptr, stream);
+}
+
+hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream) {
+    const int nt_tot = ka.n_terms * ka.n_ctx_eff;
+    for (int s = 0; s < st.nsteps; s++) {
+        hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
+        double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
+        hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(st.W), dim3(NT_DEFAULT), lds, stream, ka, st);
-    } else {
-        auto k = step_kernel<NT_DEFAULT, false>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(st.W), dim3(NT_DEFAULT), lds, stream, ka, st);
+        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot);
     }
     return hipGetLastError();
 }
 
 }  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps(unsigned long long *out, int reset) {  // [16][16]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps), sizeof(adx::g_stamps)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libaddapt_gpu.so")
+LIB_PATH = os.environ.get("ADX_LIB") or os.path.join(HERE, "_lib", "libaddapt_gpu.so")
 DEFAULT_PARAMS = os.path.join(HERE, "data", "rna_turner2004_addapt.par")
 
 OK, EINVAL, EHIP, ECONSTRAINT, EPARAM, ENOMEM, EMOVE, ESTATE, ENODEV, EUNSUPPORTED = range(10)

@@ -1,0 +1,97 @@
+"""Algorithmic work of one McCaskill inside pass (for bench.py's roofline).
+
+FLOPs per partition function (DESIGN.md "Roofline"):
+  3 per interior-loop term  qb[p][q] * f(i,j,p,q) accumulated, counted for
+                            every pair of pairable cells (i,j) ⊃ (p,q) with
+                            n1 + n2 <= 30 allowed by the hard constraint;
+  2 per multiloop-closing term qm[i+1][k-1] * qm1[k][j-1], k in [i+6, j-5],
+                            for every pairable (i,j);
+  2 per qm split term       (pre + qm[i][k-1]) * qm1[k][j], k in [i, j-4],
+                            for every cell (i,j) with 4 <= j-i <= N-6.
+Exterior, hairpin and O(1)-per-cell work are not counted.  Pure numpy, no
+oracle (the product may not call the checker).
+"""
+import numpy as np
+
+PAIR = np.zeros((5, 5), dtype=np.int8)
+for a, b, t in ((2, 3, 1), (3, 2, 2), (3, 4, 3), (4, 3, 4), (1, 4, 5), (4, 1, 6)):
+    PAIR[a, b] = t
+CODE = {"A": 1, "C": 2, "G": 3, "U": 4, "T": 4}
+
+
+def _hc(cst, N):
+    """allowed[i][j] (1-based) and up/dn runs for a dot-bracket constraint."""
+    partner = np.zeros(N + 2, dtype=np.int64)
+    enc = np.zeros(N + 2, dtype=np.int64)
+    unp = np.ones(N + 2, dtype=bool)
+    flg = np.zeros(N + 2, dtype=np.int64)
+    stk = []
+    for i in range(1, N + 1):
+        c = cst[i - 1] if cst else "."
+        enc[i] = stk[-1] if stk else 0
+        if c == "(":
+            stk.append(i)
+        elif c == ")":
+            a = stk.pop()
+            partner[a], partner[i] = i, a
+            enc[i] = stk[-1] if stk else 0
+        if c == "x":
+            flg[i] |= 1
+        if c == "<":
+            flg[i] |= 2
+        if c == ">":
+            flg[i] |= 4
+        if c in "|<>" or c in "()":
+            unp[i] = False
+    I = np.arange(N + 2)[:, None]
+    J = np.arange(N + 2)[None, :]
+    fi, fj = flg[:, None], flg[None, :]
+    ok = ((fi | fj) & 1) == 0
+    ok &= (fi & 2) == 0
+    ok &= (fj & 4) == 0
+    pi, pj = partner[:, None], partner[None, :]
+    ok &= np.where(pi > 0, pi == J, np.where(pj > 0, pj == I, enc[:, None] == enc[None, :]))
+    up = np.zeros(N + 3, dtype=np.int64)
+    for i in range(N, 0, -1):
+        up[i] = up[i + 1] + 1 if unp[i] else 0
+    dn = np.zeros(N + 2, dtype=np.int64)
+    for i in range(1, N + 1):
+        dn[i] = dn[i - 1] + 1 if unp[i] else 0
+    return ok, up, dn
+
+
+def pf_terms(seq, cst=None):
+    """(interior terms, multiloop terms) of one inside pass."""
+    N = len(seq)
+    S = np.zeros(N + 2, dtype=np.int64)
+    S[1:N + 1] = [CODE.get(c.upper(), 0) for c in seq]
+    ok, up, dn = _hc(cst, N)
+    I = np.arange(N + 2)[:, None]
+    J = np.arange(N + 2)[None, :]
+    pairable = (PAIR[S[:, None], S[None, :]] > 0) & ok & (J - I >= 4)
+    pairable[0, :] = pairable[:, 0] = False
+    pairable[N + 1, :] = pairable[:, N + 1] = False
+    n_int = 0
+    ii, jj = np.nonzero(pairable)
+    for i, j in zip(ii, jj):
+        for n1 in range(0, 31):
+            p = i + 1 + n1
+            if p >= j - 4 or (n1 > 0 and up[i + 1] < n1):
+                break
+            n2max = min(30 - n1, j - 1 - (p + 4))
+            if n2max < 0:
+                continue
+            qs = np.arange(j - 1, j - 2 - n2max, -1)
+            n2s = j - 1 - qs
+            valid = (n2s == 0) | (dn[j - 1] >= n2s)
+            n_int += int(np.count_nonzero(pairable[p, qs] & valid))
+    d = jj - ii
+    n_ml = int(np.clip(d - 10, 0, None).sum())
+    dd = np.arange(4, max(4, N - 5))
+    n_ml += int(((N - dd) * (dd - 3)).sum())
+    return n_int, n_ml
+
+
+def pf_flops(seq, cst=None):
+    a, b = pf_terms(seq, cst)
+    return 3 * a + 2 * b

@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark: MC steps/s (fold + score + accept), 100-nt sgRNA, 4096 walkers per GPU.
+
+A "step" is one MonteCarlo::apply iteration (sampling.cc:55-99) for every
+walker of the batch: thermostat, mutation move, and -- when the sequence
+changed -- the default objective's 4 McCaskill partition functions
+(apo/holo x unconstrained/"active", scoring.cc:145-146, 58, 65) and the
+Metropolis test.  ACCEPT_UNCHANGED steps count, as in the reference counters.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 4096] [--length 100]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; walkers are
+sharded (weak scaling, global walker id = rank * W + w), no collective on
+the data path; a barrier + max-over-ranks brackets the timed region.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MC steps/sec (fold+score+accept), 100-nt sgRNA, 4096 walkers, 1/8 GPU"
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix rate
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--walkers", type=int, default=4096)
+    ap.add_argument("--length", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="approximate budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_traffic.py) to fill roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(tmpl, active, walker_seqs, budget_s):
+    """Oracle MC (the C++-equivalent CPU restatement, 'port') on the host cores."""
+    from oracle import oracle as O
+    from addapt_amd import workloads
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+    sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
+    th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    # probe: 1 walker x 4 steps on one thread to size the sample
+    t_probe, _ = O.mc_run_batch(sf, walker_seqs[:1], [active], th, [0], 4, 1)
+    per_step = max(t_probe / 4.0, 1e-4)
+    steps = 8
+    walkers = max(threads, int(budget_s * threads / (per_step * steps)))
+    walkers = min(walkers, len(walker_seqs))
+    walkers = max(threads, (walkers // threads) * threads)
+    seqs = walker_seqs[:walkers]
+    t, counters = O.mc_run_batch(sf, seqs, [active], th, list(range(walkers)), steps, threads)
+    total = walkers * steps
+    return {"value": total / t, "unit": "MC steps/s", "cores": threads, "kind": "port",
+            "sample": "%d walkers x %d steps of the same workload (oracle/ C restatement of "
+                      "MonteCarlo::apply + ViennaRNA pf, FP64, 1 walker per OpenMP thread), %.1f s"
+                      % (walkers, steps, t),
+            "per_core": total / t / threads,
+            "reference_2016_per_core": 14.4}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_
+
+        torch.cuda.set_device(local_rank)
+        dist_.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = dist_
+
+    from addapt_amd import native, roofline, workloads
+
+    tmpl, active = workloads.synthetic(a.length)
+    terms = workloads.default_objective()
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank)
+    W = a.walkers
+    gids = [rank * W + w for w in range(W)]
+    seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + rank * W)
+    eng.walkers_init(gids, seqs)
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    if a.warmup > 0:
+        eng.run_steps(a.warmup)
+    _, _, c0 = eng.download()
+    barrier()
+    t0 = time.perf_counter()
+    eng.run_steps(a.steps)
+    barrier()
+    t1 = time.perf_counter()
+    kernel_ms = eng.last_kernel_ms()
+    _, _, c1 = eng.download()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps_total = W * a.steps * world
+    value = steps_total / elapsed
+
+    # algorithmic FLOPs of the launch: scored steps x sum over the PF variants
+    dc = c1 - c0
+    scored = int(dc[:, 0].sum() + dc[:, 1].sum() + dc[:, 3].sum())
+    sample = [tmpl] + seqs[:7]
+    f_free = sum(roofline.pf_flops(s, None) for s in sample) / len(sample)
+    f_act = sum(roofline.pf_flops(s, active) for s in sample) / len(sample)
+    flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
+    launch_flops = scored * flop_per_scored
+    achieved_tflops = launch_flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else None
+    traffic = None
+    if a.traffic_json and os.path.exists(a.traffic_json):
+        with open(a.traffic_json) as f:
+            traffic = json.load(f).get("bytes_per_launch")
+    roof = {
+        "bound": "mfma",
+        "achieved": achieved_tflops,
+        "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": (achieved_tflops / FP32_PEAK_TFLOPS) if achieved_tflops else None,
+        "traffic": traffic,
+        "compute_unit": "fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
+                        "products, not a contraction); peak = gfx950 fp32 rate, vector == matrix",
+        "kernel": "step_kernel<512,qbm>",
+        "kernel_ms_per_launch": kernel_ms,
+        "flop_per_scored_step": flop_per_scored,
+        "scored_steps_in_launch": scored,
+        "hbm_algorithmic_GBps": (scored * (4 * 100 + 8) + W * a.steps * 16) / (kernel_ms * 1e-3) / 1e9
+        if kernel_ms > 0 else None,
+    }
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "MC steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {
+            "workload": "default objective (apo: not active, holo: active; THEO aptamer 0.32 uM): "
+                        "4 McCaskill inside PFs per scored step, synthetic %d-nt sgRNA template "
+                        "(SURVEY.md 8d), %d walkers per GPU, annealing 5 to 0 in 300 steps"
+                        % (a.length, W),
+            "walkers_per_gpu": W,
+            "global_walkers": W * world,
+            "length": a.length,
+            "parallelism": "walker-sharded x%d (no data-path collective)" % world,
+            "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, dc.sum(axis=0))},
+        },
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
