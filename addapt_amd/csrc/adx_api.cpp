@@ -202,7 +202,7 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
     ct[CT_FSM + 4] = static_cast<float>(sp(6));
     ct[CT_FSM + 5] = static_cast<float>(boltz_d(P.interior[5] + P.ninio) * sp(7));
     ct[CT_FSM + 6] = static_cast<float>(boltz_d(P.TermAU));
-    ct[CT_FSM + 7] = 0.f;
+    ct[CT_ONE] = 1.f;
     for (int u = 6; u <= MAXLOOP; u++)
         for (int n1 = 2; n1 < 2 + FG_ROW; n1++) {
             const int n2 = u - n1;
@@ -211,6 +211,35 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
                 f = boltz_d(P.interior[u] + std::min(P.maxninio, std::abs(n1 - n2) * P.ninio)) * sp(u + 2);
             X.fgen[(u - 6) * FG_ROW + n1 - 2] = static_cast<float>(f);
         }
+    // term lists ordered by u (dev_types.hpp NS_MAX)
+    int ns = 0, ng = 0;
+    auto addS = [&](int kind, int n1, int n2, float f) {
+        X.s_kind[ns] = static_cast<uint8_t>(kind);
+        X.s_n1[ns] = static_cast<uint8_t>(n1);
+        X.s_n2[ns] = static_cast<uint8_t>(n2);
+        X.s_f[ns] = f;
+        ns++;
+    };
+    for (int u = 0; u <= MAXLOOP; u++) {
+        if (u == 0) addS(TK_STK, 0, 0, ct[CT_FSM + 0]);
+        if (u == 1) { addS(TK_B1, 0, 1, ct[CT_FSM + 1]); addS(TK_B1, 1, 0, ct[CT_FSM + 1]); }
+        if (u == 2) addS(TK_I11, 1, 1, ct[CT_FSM + 2]);
+        if (u == 3) { addS(TK_I12, 1, 2, ct[CT_FSM + 3]); addS(TK_I21, 2, 1, ct[CT_FSM + 3]); }
+        if (u == 4) addS(TK_I22, 2, 2, ct[CT_FSM + 4]);
+        if (u == 5) { addS(TK_M23, 2, 3, ct[CT_FSM + 5]); addS(TK_M23, 3, 2, ct[CT_FSM + 5]); }
+        if (u >= 2) { addS(TK_BUL, 0, u, ct[CT_FB + u]); addS(TK_BUL, u, 0, ct[CT_FB + u]); }
+        if (u >= 4) { addS(TK_1N, 1, u - 1, ct[CT_F1N + u - 1]); addS(TK_1N, u - 1, 1, ct[CT_F1N + u - 1]); }
+        for (int n1 = 2; u >= 6 && n1 <= u - 2; n1++) {
+            X.g_n1[ng] = static_cast<uint8_t>(n1);
+            X.g_u[ng] = static_cast<uint8_t>(u);
+            X.g_f[ng] = X.fgen[(u - 6) * FG_ROW + n1 - 2];
+            ng++;
+        }
+        X.s_cnt[u] = ns;
+        X.g_cnt[u] = ng;
+    }
+    X.s_cnt[31] = ns;
+    X.g_cnt[31] = ng;
     for (int k = 0; k < NMAX + 4; k++) X.sig[k] = static_cast<float>(sp(k));
     for (int u = 0; u <= NMAX; u++) {
         double e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + P.lxc * std::log(u / 30.0);
@@ -220,21 +249,21 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
     for (int t = 0; t <= NMAX; t++) X.pwml[t] = static_cast<float>(std::pow(mlb * sigma, t));
     X.mlclosing = static_cast<float>(boltz_d(P.MLclosing) * sp(2));
     X.mlbase_sig = static_cast<float>(mlb * sigma);
-    int ns = 0;
+    int nsp = 0;
     auto add_special = [&](const std::vector<std::pair<std::string, int>> &tab) {
         for (auto &e : tab) {
-            if (ns >= MAX_SPECIAL_HP) break;
+            if (nsp >= MAX_SPECIAL_HP) break;
             std::vector<uint8_t> codes(e.first.size());
             for (size_t k = 0; k < e.first.size(); k++) codes[k] = static_cast<uint8_t>(base_code(e.first[k]));
-            X.sp_key[ns] = hp_key(codes.data(), 0, static_cast<int>(codes.size()));
-            X.sp_val[ns] = static_cast<float>(boltz_d(e.second) * sp(static_cast<int>(codes.size())));
-            ns++;
+            X.sp_key[nsp] = hp_key(codes.data(), 0, static_cast<int>(codes.size()));
+            X.sp_val[nsp] = static_cast<float>(boltz_d(e.second) * sp(static_cast<int>(codes.size())));
+            nsp++;
         }
     };
     add_special(P.triloops);
     add_special(P.tetraloops);
     add_special(P.hexaloops);
-    X.n_special = ns;
+    X.n_special = nsp;
     X.log_sigma = std::log(sigma);
     X.kT = kT_kcal();
     if (m.present) {

@@ -33,11 +33,23 @@ constexpr int CT_STK = 800;    // [8][8] stack
 constexpr int CT_FB = 864;     // [n]   bulge n: exp(-bulge[n]) * sigma^(n+2)
 constexpr int CT_F1N = 896;    // [nl]  1 x nl: exp(-(interior[nl+1] + ninio)) * sigma^(nl+3)
 constexpr int CT_FSM = 928;    // [0] s^2 [1] bulge1 s^3 [2] s^4 [3] s^5 [4] s^6 [5] 2x3 s^7 [6] exp(-TermAU)
+constexpr int CT_ONE = 935;    // 1.0 (neutral second factor)
 constexpr int CT_SIZE = 936;
 // generic interior factors exp(-(interior[u] + ninio)) * sigma^(u+2) for
 // u = 6..30, n1 = 2..28: DevScaled::fgen[(u - 6) * FG_ROW + n1 - 2]
 constexpr int FG_ROW = 27;
 constexpr int FG_SIZE = 25 * FG_ROW;
+
+// Interior-loop term lists of one closing pair (i,j), ordered by loop size
+// u = n1 + n2 so that the terms allowed at a span (u <= min(30, span-6)) are a
+// prefix.  The kernel maps term t of a list to lane t % 64 of slot t / 64.
+//   S list: every loop whose factor depends on the inner pair (stack, bulges,
+//           1x1 / 1x2 / 2x1 / 2x2 tables, 2x3 mismatches, 1 x n loops), <= 121
+//   G list: generic loops n1, n2 >= 2, u >= 6 (factor fgen, inner mismatch
+//           folded into qbm), <= 375
+constexpr int NS_MAX = 128;
+constexpr int NG_MAX = 384;
+enum TermKind : uint8_t { TK_STK = 0, TK_B1, TK_I11, TK_I12, TK_I21, TK_I22, TK_M23, TK_BUL, TK_1N };
 
 struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
     float stack[8][8];
@@ -55,7 +67,13 @@ struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
 
 struct DevScaled {
     float ctab[CT_SIZE];     // see CT_* (copied to LDS)
-    float fgen[FG_SIZE];     // generic interior factors (copied to LDS)
+    float fgen[FG_SIZE];     // generic interior factors
+    // interior term lists (see NS_MAX); *_cnt[umax] = terms with u <= umax
+    uint8_t s_n1[NS_MAX], s_n2[NS_MAX], s_kind[NS_MAX];
+    float s_f[NS_MAX];       // constant factor (sigma power, bulge / 1xn length)
+    uint8_t g_n1[NG_MAX], g_u[NG_MAX];
+    float g_f[NG_MAX];
+    int s_cnt[32], g_cnt[32];
     float sig[NMAX + 4];     // sigma^k
     float hp[NMAX + 1];      // hairpin length factor * sigma^(u+2)
     float pwml[NMAX + 1];    // (expMLbase * sigma)^t

@@ -55,6 +55,14 @@ __device__ __forceinline__ float dpp_add(float v) {
     const int moved = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false);
     return v + __int_as_float(moved);
 }
+// Sum over each row of 16 lanes; the row total lands in lane 15 of the row.
+__device__ __forceinline__ float row_sum(float v) {
+    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    return v;
+}
 __device__ __forceinline__ float wave_sum(float v) {
     v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
     v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
@@ -98,64 +106,78 @@ constexpr int DT_MMI = 200;    // [type][x][y] interior mismatch
 constexpr int DT_MLS = 400;    // [type][x][y] multiloop stem
 constexpr int DT_EXT = 600;    // [type][6][6] exterior stem
 constexpr int DT_TAU = 888;    // [type] terminal AU
-constexpr int DT_SPK = 896;    // special hairpin keys (bit patterns)
-constexpr int DT_SPV = DT_SPK + MAX_SPECIAL_HP;
-constexpr int DT_HP = DT_SPV + MAX_SPECIAL_HP;  // [u] hairpin length factor
+constexpr int DT_HP = 896;     // [u] hairpin length factor
 
-// LDS carve-out for one workgroup (see lds_bytes()).
+constexpr int CHUNK = 16;      // closing-pair cells per chunk of one wave (4 prefetch lanes each)
+constexpr int GSLOTS = NG_MAX / WAVE;   // 6
+constexpr int SSLOTS = NS_MAX / WAVE;   // 2
+constexpr int QSLOTS = (NMAX + 1 + WAVE - 1) / WAVE;  // 4
+
+// LDS carve-out for one workgroup.  lds_layout() is the single source of the
+// layout: the kernel carves with it and the host sizes the launch with it.
 struct Lds {
     float *qbm, *qm, *qm1;
     uint8_t *cc;       // inner-pair code per cell (diagonal-major)
-    float *scr;        // 2 x NT floats (double-buffered partial rows) + 4 q5 partials
+    uint8_t *pcnt;     // [d] pairable cells of diagonal d
+    uint8_t *wsc;      // [wave][64] i of the cells of a wave's chunk
+    float *mla;        // [2][np] sum_k qm[i][k-1] qm1[k][j] of the last two qm diagonals
     float *ct;         // CT_SIZE factor table (DevScaled::ctab)
-    float *dt;         // LDS copy of per-cell tables (DT_*)
+    float *dt;         // per-cell tables (DT_*)
     float *q5;
-    float *misc;       // [0] = q5 partial
+    uint16_t *gd;      // G list: n1 | n2 << 8        (NG_MAX)
+    float *gf;         // G list factors               (NG_MAX)
+    uint32_t *sd;      // S list: n1 | n2 << 8 | kind << 16 (NS_MAX)
+    float *sf;         // S list factors               (NS_MAX)
+    float *pw;         // (expMLbase sigma)^t          (Nmax + 1)
     double *G;         // per-variant ensemble energies
-    uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat;
-    uint8_t *lists;    // plist[4] then pinv[4], NP bytes each
+    uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
     int np;
-    int *pcount;       // [2]
-    uint8_t *raw;      // scored sequence (Nraw)
 };
 
-template <int NT>
-__device__ Lds carve(char *base, const KArgs &ka) {
-    Lds L;
-    const int C = ka.cells;
+// DRY = true: sizes only (host); false: carve `base` (device; no null test, so
+// the pointers stay in the LDS address space)
+template <bool DRY>
+__host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, int nvar, Lds *L) {
     size_t o = 0;
-    auto take = [&](size_t bytes) {
-        char *p = base + o;
+    auto take = [&](size_t bytes) -> char * {
+        char *p = DRY ? nullptr : base + o;
         o += (bytes + 15) & ~size_t(15);
         return p;
     };
-    L.qbm = reinterpret_cast<float *>(take(size_t(C) * 4));
-    L.qm = reinterpret_cast<float *>(take(size_t(C) * 4));
-    L.qm1 = reinterpret_cast<float *>(take(size_t(C) * 4));
-    L.cc = reinterpret_cast<uint8_t *>(take(size_t(C)));
-    L.scr = reinterpret_cast<float *>(take(2 * NT * 4 + 16));
-    L.ct = reinterpret_cast<float *>(take(CT_SIZE * 4));
-    L.dt = reinterpret_cast<float *>(take(size_t(DT_HP + ka.Nmax + 1) * 4));
-    const int NP = ka.Nmax + 2;
-    L.q5 = reinterpret_cast<float *>(take(NP * 4));
-    L.misc = reinterpret_cast<float *>(take(16 * 4));
-    L.G = reinterpret_cast<double *>(take(ka.n_variants * 8));
-    L.pcount = reinterpret_cast<int *>(take(4 * 4));
-    L.S = reinterpret_cast<uint8_t *>(take(NP));
-    L.up = reinterpret_cast<uint8_t *>(take(NP));
-    L.dn = reinterpret_cast<uint8_t *>(take(NP));
-    L.ptn = reinterpret_cast<uint8_t *>(take(NP));
-    L.enc = reinterpret_cast<uint8_t *>(take(NP));
-    L.flg = reinterpret_cast<uint8_t *>(take(NP));
-    L.mat = reinterpret_cast<uint8_t *>(take(NP));
-    L.np = NP;
-    L.lists = reinterpret_cast<uint8_t *>(take(8 * NP));
-    L.raw = reinterpret_cast<uint8_t *>(take(NP));
-    return L;
+    const size_t C = size_t(cells);
+    const int NP = Nmax + 2;
+    Lds l;
+    l.qbm = reinterpret_cast<float *>(take(C * 4));
+    l.qm = reinterpret_cast<float *>(take(C * 4));
+    l.qm1 = reinterpret_cast<float *>(take(C * 4));
+    l.cc = reinterpret_cast<uint8_t *>(take(C));
+    l.pcnt = reinterpret_cast<uint8_t *>(take(NP));
+    l.wsc = reinterpret_cast<uint8_t *>(take(16 * WAVE));
+    l.mla = reinterpret_cast<float *>(take(2 * NP * 4));
+    l.ct = reinterpret_cast<float *>(take(CT_SIZE * 4));
+    l.dt = reinterpret_cast<float *>(take(size_t(DT_HP + Nmax + 1) * 4));
+    l.q5 = reinterpret_cast<float *>(take(NP * 4));
+    l.gd = reinterpret_cast<uint16_t *>(take(NG_MAX * 2));
+    l.gf = reinterpret_cast<float *>(take(NG_MAX * 4));
+    l.sd = reinterpret_cast<uint32_t *>(take(NS_MAX * 4));
+    l.sf = reinterpret_cast<float *>(take(NS_MAX * 4));
+    l.pw = reinterpret_cast<float *>(take(size_t(Nmax + 1) * 4));
+    l.G = reinterpret_cast<double *>(take(size_t(nvar) * 8));
+    l.S = reinterpret_cast<uint8_t *>(take(NP));
+    l.up = reinterpret_cast<uint8_t *>(take(NP));
+    l.dn = reinterpret_cast<uint8_t *>(take(NP));
+    l.ptn = reinterpret_cast<uint8_t *>(take(NP));
+    l.enc = reinterpret_cast<uint8_t *>(take(NP));
+    l.flg = reinterpret_cast<uint8_t *>(take(NP));
+    l.mat = reinterpret_cast<uint8_t *>(take(NP));
+    l.raw = reinterpret_cast<uint8_t *>(take(NP));
+    l.np = NP;
+    if (!DRY) *L = l;
+    return o;
 }
 
-template <int NT>
 __device__ void load_ctab(const KArgs &ka, const Lds &L) {
+    const int NT = blockDim.x;
     for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = ka.X->ctab[k];
     const DevTables &T = *ka.T;
     const DevScaled &X = *ka.X;
@@ -166,15 +188,19 @@ __device__ void load_ctab(const KArgs &ka, const Lds &L) {
     }
     for (int k = threadIdx.x; k < 288; k += NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
     for (int k = threadIdx.x; k < 8; k += NT) L.dt[DT_TAU + k] = T.termAU[k];
-    for (int k = threadIdx.x; k < MAX_SPECIAL_HP; k += NT) {
-        L.dt[DT_SPK + k] = __uint_as_float(k < X.n_special ? X.sp_key[k] : 0u);
-        L.dt[DT_SPV + k] = X.sp_val[k];
+    for (int k = threadIdx.x; k <= ka.Nmax; k += NT) {
+        L.dt[DT_HP + k] = X.hp[k];
+        L.pw[k] = X.pwml[k];
     }
-    for (int k = threadIdx.x; k <= ka.Nmax; k += NT) L.dt[DT_HP + k] = X.hp[k];
+    for (int k = threadIdx.x; k < NG_MAX; k += NT) {
+        L.gd[k] = static_cast<uint16_t>(X.g_n1[k] | ((X.g_u[k] - X.g_n1[k]) << 8));
+        L.gf[k] = X.g_f[k];
+    }
+    for (int k = threadIdx.x; k < NS_MAX; k += NT) {
+        L.sd[k] = uint32_t(X.s_n1[k]) | (uint32_t(X.s_n2[k]) << 8) | (uint32_t(X.s_kind[k]) << 16);
+        L.sf[k] = X.s_f[k];
+    }
 }
-
-__device__ __forceinline__ uint8_t *plist(const Lds &L, int b) { return L.lists + b * L.np; }
-__device__ __forceinline__ uint8_t *pinv(const Lds &L, int b) { return L.lists + (4 + b) * L.np; }
 
 // ---------------------------------------------------------------- hard constraints
 // flg bits: 1 = 'x' (no pair), 2 = '<' (pairs upstream), 4 = '>' (downstream);
@@ -189,54 +215,175 @@ __device__ __forceinline__ bool allowed(const Lds &L, int i, int j) {
     return L.enc[i] == L.enc[j];
 }
 
-__device__ __forceinline__ bool pairable(const Lds &L, int i, int j) {
-    return ptype(L.S[i], L.S[j]) != 0 && allowed(L, i, j);
+// ceil(x / y) for 0 < y, |x| < 2^22 (uniform operands; float reciprocal + exact fix-up,
+// the scalar unit has no integer divide)
+__device__ __forceinline__ int cdiv_pos(int x, int y) {
+    if (x <= 0) return 0;
+    int q = static_cast<int>(static_cast<float>(x) * __builtin_amdgcn_rcpf(static_cast<float>(y)));
+    if (q * y < x) q++;
+    if (q * y < x) q++;
+    if ((q - 1) * y >= x) q--;
+    return uni(q);
+}
+__device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// ---------------------------------------------------------------- closing-pair terms
+// Per-lane descriptors of one span's interior-loop terms (lane t of slot s =
+// term s*64 + t of the S / G lists, dev_types.hpp).  Invalid lanes carry offset
+// 0 (a finished cell) and factor 0.
+struct TermLanes {
+    int offG[GSLOTS];      // qbm index of the inner cell minus i
+    float fG[GSLOTS];
+    int offS[SSLOTS];
+    float fS[SSLOTS];
+    int b1[SSLOTS];        // ct base of the inner-pair factor (INVMM / BUL / ONEN)
+    int b2;                // slot 0: ct base of the second factor (STK / M23O / ONE)
+    int mwt, mwc;          // slot 0: all-ones masks adding ty*8+t2 (stack) / code (2x3)
+    float eb, em, e3, eg;  // slot 0: 0/1 selectors of tau, mo, m23 and the table factor
+    float em1;             // slot 1: 1 = 1xn (mo), 0 = bulge (tau)
+    int gsel;              // slot 0: which prefetched table factor (kind - TK_I11) & 3
+};
+
+// Uniform data of one closing pair (i, j) of the current span.
+struct CellU {
+    int i, ty8, A, B;
+    float mmo, tau, mo, m23;
+};
+
+// Sum of the interior-loop terms of (i, j) (before the outer mismatch of the
+// generic loops, which is applied here): SS / SG slots, MK = constrained cell.
+template <int SS, int SG, bool MK>
+__device__ __forceinline__ float qb_terms(const Lds &L, const TermLanes &D, const CellU &u, float gtab) {
+    if (SS == 0) return 0.f;
+    const float *ct = L.ct;
+    const int lane = threadIdx.x & (WAVE - 1);
+    float q[SG > 0 ? SG : 1];
+#pragma unroll
+    for (int s = 0; s < SG; s++) q[s] = L.qbm[D.offG[s] + u.i];
+    const int ix0 = D.offS[0] + u.i;
+    const float qs0 = L.qbm[ix0];
+    const int c0 = L.cc[ix0];
+    float qs1 = 0.f;
+    int c1 = 0;
+    if (SS > 1) {
+        const int ix1 = D.offS[1] + u.i;
+        qs1 = L.qbm[ix1];
+        c1 = L.cc[ix1];
+    }
+    float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+    for (int s = 0; s < SG; s++) {
+        float f = D.fG[s];
+        if (MK) {   // constrained cell: n1 <= A and n2 <= B (descriptor re-read from LDS)
+            const int pk = L.gd[s * WAVE + lane];
+            f = ((pk & 255) <= u.A && (pk >> 8) <= u.B) ? f : 0.f;
+        }
+        if (s & 1) g1 = fmaf(q[s], f, g1);
+        else g0 = fmaf(q[s], f, g0);
+    }
+    // slot 0: stack / bulge 1 / 1x1..2x2 tables / 2x3 / bulges / 1xn
+    const int t2 = (c0 * 41) >> 10;
+    const int i2 = D.b2 + ((u.ty8 + t2) & D.mwt) + (c0 & D.mwc);
+    const float uf = fmaf(D.eb, u.tau - 1.f, fmaf(D.em, u.mo - 1.f, fmaf(D.e3, u.m23 - 1.f, 1.f)));
+    const float gf = fmaf(D.eg, gtab - 1.f, 1.f);
+    float f0 = ct[D.b1[0] + c0] * ct[i2] * (D.fS[0] * uf) * gf;
+    if (MK) {
+        const int pk = int(L.sd[lane]);
+        f0 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f0 : 0.f;
+    }
+    float sa = qs0 * f0;
+    if (SS > 1) {
+        // slot 1: bulges and 1xn only
+        float f1 = ct[D.b1[1] + c1] * (D.fS[1] * fmaf(D.em1, u.mo - u.tau, u.tau));
+        if (MK) {
+            const int pk = int(L.sd[WAVE + lane]);
+            f1 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f1 : 0.f;
+        }
+        sa = fmaf(qs1, f1, sa);
+    }
+    return fmaf(g0 + g1, u.mmo, sa);
 }
 
-// one wave: compact the pairable cells of diagonal dd into buffer b
-__device__ void build_plist(const Lds &L, int N, int dd, int b, int lane) {
-    const int c = N - dd;
-    int base = 0;
-    for (int r0 = 0; r0 < c; r0 += WAVE) {
-        const int r = r0 + lane;
-        const int i = r + 1;
-        const bool valid = r < c;
-        const bool f = valid && pairable(L, i, i + dd);
-        const unsigned long long m = __ballot(f);
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        if (f) {
-            plist(L, b)[base + rank] = static_cast<uint8_t>(i);
-            pinv(L, b)[i] = static_cast<uint8_t>(base + rank);
-        } else if (valid) {
-            pinv(L, b)[i] = 0xFF;
+template <bool MK>
+__device__ __forceinline__ float qb_terms_dispatch(int sS, int sG, const Lds &L, const TermLanes &D,
+                                                   const CellU &u, float gtab) {
+    if (sS == 2) {
+        switch (sG) {
+            case 6: return qb_terms<2, 6, MK>(L, D, u, gtab);
+            case 5: return qb_terms<2, 5, MK>(L, D, u, gtab);
+            case 4: return qb_terms<2, 4, MK>(L, D, u, gtab);
+            case 3: return qb_terms<2, 3, MK>(L, D, u, gtab);
+            default: return qb_terms<2, 2, MK>(L, D, u, gtab);
         }
-        base += __popcll(m);
     }
-    if (lane == 0) L.pcount[b] = base;
+    if (sS == 1) {
+        switch (sG) {
+            case 0: return qb_terms<1, 0, MK>(L, D, u, gtab);
+            case 1: return qb_terms<1, 1, MK>(L, D, u, gtab);
+            default: return qb_terms<1, 2, MK>(L, D, u, gtab);
+        }
+    }
+    return 0.f;
+}
+
+// qm(i, i+sq) split sums over SQ slots of split points t (lanes):
+//   A = sum_{t>=5} qm[i][i+t-1] qm1[i+t][jb],  P = sum_t pw(t) qm1[i+t][jb]
+template <int SQ>
+__device__ __forceinline__ void qm_terms(const float *q1, const float *qr, int tmax, int upi,
+                                         const float *pwr, int lane, float &A, float &P) {
+    float v1[SQ], vr[SQ];
+#pragma unroll
+    for (int q = 0; q < SQ; q++) {
+        const int t = q * WAVE + lane;
+        v1[q] = q1[t <= tmax ? t : tmax];
+        vr[q] = qr[(t <= tmax && t >= 5) ? t : 5];
+    }
+    float a0 = 0.f, p0 = 0.f;
+#pragma unroll
+    for (int q = 0; q < SQ; q++) {
+        const int t = q * WAVE + lane;
+        const bool ok = t <= tmax;
+        const float b = ok ? v1[q] : 0.f;
+        a0 = fmaf((ok && t >= 5) ? vr[q] : 0.f, b, a0);
+        p0 = fmaf((ok && t <= upi) ? pwr[q] : 0.f, b, p0);
+    }
+    A = a0;
+    P = p0;
 }
 
 // ---------------------------------------------------------------- inside PF
-// Per-diagonal pipeline with ONE barrier per iteration d:
-//   jobs (all waves, lanes = cells):  A  qb(d) partials      (reads spans <= d-2)
-//                                     B  qm(d-2) partials    (qm1 span d-2, qm <= d-7)
-//                                     C  q5[d-1] partial     (qb spans <= d-2)
-//   finalize (one item per thread):   qb(d-1) + qbm/code + qm1(d-1), qm(d-3), q5[d-2],
-//                                     from the partials iteration d-1 left in the other
-//                                     scratch buffer; plus the pairable list of d+1.
-// qb(d) never reads span d-1 (stack = span d-2), so the finalize of d-1 and the
-// partials of d share one phase.
+// Per-variant setup pass (all cells at once, no DP dependency):
+//   cc    inner-pair code of every cell,
+//   qbm   hairpin (+ ligand motif) factor of every pairable cell, 0 otherwise,
+//   qm1   multiloop-stem factor of every pairable cell, 0 otherwise,
+//   pcnt  the number of pairable cells of every diagonal.
+// A non-pairable cell keeps qbm = -0.0f for the whole fold (it is never
+// finalized, and adds 0 wherever it is read); a wave finds the pairable cells
+// of its share of a diagonal by a ballot scan of that sign bit.
+// Main loop, ONE barrier per iteration d = 4..N.  Items of iteration d:
+//   qb(i, i+d) for the pairable cells   reads qbm spans <= d-2, mla(d-2), qm1(d-1)
+//   qm(i, i+d-1) + mla(d-1)             reads qm1 spans <= d-1, qm spans <= d-6
+//   q5[d]                               reads qbm spans <= d-1, q5 <= d-1
+//   qm1 of the non-pairable cells of d  reads qm1(d-1)
+// A closing-pair cell is summed by ONE wave: lanes = terms of its interior-loop
+// lists (S and G, dev_types.hpp), reduced with DPP; its multiloop term is the
+// split sum mla(i+1, j-1) that the qm item of the previous iteration kept.  A qm
+// item is one wave as well (lanes = split points).  Items are cut into NW
+// contiguous ranges of equal estimated cost, one per wave.
 template <int NT>
-__device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds &L,
-                           const DevScaled *__restrict__ XS) {
+__device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds &L,
+                           const DevScaled *__restrict__ XS0) {
     constexpr int NW = NT / WAVE;
+    // opaque copies: keep the compiler from hoisting dozens of derived 64-bit
+    // addresses out of the variant loop (they spill SGPRs)
+    const DevScaled *__restrict__ XS = XS0;
     const DevVariant V = ka.variants[v];
-    const int N = V.N;
-    const DevTables &T = *ka.T;
-    const DevScaled &X = *ka.X;
+    const int N = uni(V.N);
     const float *ct = L.ct;
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int wid = uni(tid / WAVE);
+    const int NP = L.np;
 
     // ---- per-variant setup: sequence, constraint arrays, motif sites
     const uint8_t *cons = ka.cons + V.cons_off;
@@ -267,22 +414,22 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
         L.mat[k] = 0;
         if (k >= 1 && k <= N && (f || pt)) constrained = true;
     }
+    for (int k = tid; k < 2 * NP; k += NT) L.mla[k] = 0.f;
     constrained = __syncthreads_or(constrained);
     if (tid == 0) {
         // ViennaRNA's S1 wrap-around (only reaches values that are never used)
         L.S[0] = L.S[N];
         L.S[N + 1] = L.S[1];
-        L.q5[0] = 1.0f;
     }
-    const int mL = X.motif_len;
+    const int mL = XS->motif_len;
     if (V.motif && mL > 0) {
         for (int o = tid + 1; o + mL - 1 <= N; o += NT) {
             bool ok = true;
             for (int k = 0; k < mL && ok; k++) {
-                if (L.S[o + k] != X.motif_code[k]) ok = false;
+                if (L.S[o + k] != XS->motif_code[k]) ok = false;
             }
             for (int k = 0; k < mL && ok; k++) {
-                const int pk = X.motif_pt[k];
+                const int pk = XS->motif_pt[k];
                 if (pk < 0) ok = L.up[o + k] >= 1;
                 else if (pk > k) ok = allowed(L, o + k, o + pk);
             }
@@ -290,387 +437,337 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
         }
     }
     __syncthreads();
-    const float sig1 = X.sig[1];
+    const float sig1 = XS->sig[1];
+    const float mlbase_sig = XS->mlbase_sig;
+    const float mlclosing = XS->mlclosing;
+    const float eTAU = XS->ctab[CT_FSM + 6];
+    const int mlen = V.motif ? mL : 0;
+    const float mextra = XS->motif_extra;
+    const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
     if (tid == 0) {
+        L.q5[0] = 1.0f;
         for (int j = 1; j <= 3 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] * sig1 : 0.f;
     }
-    if (wid == NW - 1 && N - 1 >= 4) build_plist(L, N, 4, 0, lane);
+    // cells of every diagonal: wave w takes diagonals 4 + w, 4 + w + NW, ...
+    for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
+        const int c = N - dd;
+        const int od = off(dd, N);
+        const int u = dd - 1;
+        int base = 0;
+        for (int r0 = 0; r0 < c; r0 += WAVE) {
+            const int r = r0 + lane;
+            const bool valid = r < c;
+            bool pr = false;
+            if (valid) {
+                const int i = r + 1, j = i + dd;
+                const int si = L.S[i], sj = L.S[j], sim = L.S[i - 1], sjp = L.S[j + 1];
+                const int type = ptype(si, sj);
+                pr = type != 0 && allowed(L, i, j);
+                float h = 0.f, m1 = 0.f;
+                if (pr) {
+                    if (L.up[i + 1] >= u) {
+                        h = -1.f;
+                        if (u == 3 || u == 4 || u == 6) {
+                            const uint32_t key = hp_key(L.S, i, u + 2);
+                            for (int k = 0; k < nsp; k++)
+                                if (XS->sp_key[k] == key) { h = XS->sp_val[k]; break; }
+                        }
+                        if (h < 0.f)
+                            h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type]
+                                                            : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
+                    }
+                    if (dd == mlen - 1 && L.mat[i]) h += mextra;
+                    m1 = L.dt[DT_MLS + type * 25 + sim * 5 + sjp];
+                }
+                L.qbm[od + r] = pr ? h : -0.0f;
+                L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
+                L.qm1[colb(j) + i - 1] = m1;
+            }
+            base += __popcll(__ballot(pr));
+        }
+        if (lane == 0) L.pcnt[dd] = static_cast<uint8_t>(base);
+    }
+
     __syncthreads();
 
-    const float mlbase_sig = X.mlbase_sig;
-    const float mlclosing = X.mlclosing;
-    const float eTAU = ct[CT_FSM + 6];
-    const int mlen = V.motif ? mL : 0;
-    const float mextra = X.motif_extra;
-    const int nsp = X.n_special < MAX_SPECIAL_HP ? X.n_special : MAX_SPECIAL_HP;
-    // split of the previous iteration (to find its partials)
-    int p_gA = 0, p_slA = 0, p_gB = 0, p_slB = 0, p_nA = 0;
+    // ---------------- loop-carried state.  prep(d) runs at the end of
+    // iteration d-1 (before its barrier) and fills everything iteration d needs
+    // that iteration d-1 does not write: item ranges, the first chunk of
+    // closing-pair cells, their table prefetch, the term descriptors.
+    const DevTables &T = *ka.T;
+    int cp = 0, cq = 0, umax = 0, sS = 0, sG = 0, nit = 0, sQ5 = 0;
+    int kb_lo = 0, kb_hi = 0, km_lo = 0, km_hi = 0;
+    // closing-pair chunk (lanes = cells of the chunk)
+    int ci = 1, cty = 0, cA = 0, cB = 0, cidx = 0, cm1 = 0;
+    float cmmo = 0.f, ctau = 1.f, cmo = 0.f, cm23 = 0.f, cmmc = 0.f, cpre = 0.f, cpm1 = 0.f, cmlc = 0.f, pfx = 0.f;
+    uint8_t *ws = L.wsc + wid * WAVE;
+    // term descriptors: offsets advance by k - d per diagonal once every term is
+    // valid (d > 36); before that they are recomputed
+    TermLanes D;
+    int kG[GSLOTS], kS[SSLOTS];
+#pragma unroll
+    for (int s = 0; s < GSLOTS; s++) {
+        const int pk = L.gd[s * WAVE + lane];
+        kG[s] = N + 3 + (pk & 255) + (pk >> 8);
+    }
+#pragma unroll
+    for (int s = 0; s < SSLOTS; s++) {
+        const int pk = int(L.sd[s * WAVE + lane]);
+        const int n1 = pk & 255, n2 = (pk >> 8) & 255, k = pk >> 16;
+        kS[s] = N + 3 + n1 + n2;
+        D.b1[s] = (k == TK_BUL) ? CT_BUL : (k == TK_1N) ? CT_ONEN : CT_INVMM;
+        if (s == 0) {
+            D.b2 = (k <= TK_B1) ? CT_STK : (k == TK_M23) ? CT_M23O : CT_ONE;
+            D.mwt = (k <= TK_B1) ? -1 : 0;
+            D.mwc = (k == TK_M23) ? -1 : 0;
+            D.eb = (k == TK_BUL) ? 1.f : 0.f;
+            D.em = (k == TK_1N) ? 1.f : 0.f;
+            D.e3 = (k == TK_M23) ? 1.f : 0.f;
+            D.eg = (k >= TK_I11 && k <= TK_I22) ? 1.f : 0.f;
+            D.gsel = (k - TK_I11) & 3;
+        } else {
+            D.em1 = (k == TK_1N) ? 1.f : 0.f;
+        }
+    }
+
+    // lanes c < nc: cell kc + c (rank among the pairable cells of diagonal d)
+    auto load_chunk = [&](int d, int kc, int nc) {
+        const int od = off(d, N);
+        {   // ballot scan of the non-pairable mark -> ws[rank - kc] = i
+            int base = 0;
+            for (int r0 = 0; r0 < N - d && base < kc + nc; r0 += WAVE) {
+                const int r = r0 + lane;
+                const bool pr = r < N - d && __float_as_uint(L.qbm[od + r]) != 0x80000000u;
+                const unsigned long long m = __ballot(pr);
+                const int rank = base + __popcll(m & ((1ull << lane) - 1ull));
+                if (pr && rank >= kc && rank < kc + nc) ws[rank - kc] = static_cast<uint8_t>(r + 1);
+                base += __popcll(m);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        {
+            const int c = lane < nc ? lane : nc - 1;
+            const int i = ws[c], j = i + d;
+            const int si1 = L.S[i + 1], sj1 = L.S[j - 1];
+            ci = i;
+            cty = ptype(L.S[i], L.S[j]);
+            cA = L.up[i + 1];
+            cB = L.dn[j - 1];
+            const int oc = cty * 25 + si1 * 5 + sj1;
+            cmmo = L.dt[DT_MMI + oc];
+            ctau = cty > 2 ? eTAU : 1.f;
+            cmo = ct[CT_ONEN + oc] * cmmo;
+            cm23 = ct[CT_M23O + oc];
+            cidx = od + i - 1;
+            cmmc = L.dt[DT_MMI + L.cc[cidx]];
+            cpre = L.qbm[cidx];
+            cm1 = colb(j) + i - 1;
+            cpm1 = L.qm1[cm1];
+            cmlc = mlclosing * L.dt[DT_MLS + rtype(cty) * 25 + sj1 * 5 + si1];
+        }
+        {   // lane 4c + g: the 1x1 / 1x2 / 2x1 / 2x2 table factor g of cell c (HBM/L2)
+            const int c = lane >> 2, g = lane & 3;
+            const int n1 = (g >= 2) ? 2 : 1, n2 = (g & 1) ? 2 : 1;
+            pfx = 0.f;
+            if (c < nc && n1 + n2 <= umax) {
+                const int i = ws[c], j = i + d;
+                const int typ = ptype(L.S[i], L.S[j]);
+                const int t2 = (L.cc[off(d - 2 - n1 - n2, N) + i + n1] * 41) >> 10;
+                const int a1 = L.S[i + 1], b1 = L.S[j - 1], sp1 = L.S[i + n1], sq1 = L.S[j - n2];
+                const float *src;
+                if (g == 0) src = &T.int11[typ][t2][a1][b1];
+                else if (g == 1) src = &T.int21[typ][t2][a1][sq1][b1];
+                else if (g == 2) src = &T.int21[t2][typ][sq1][a1][sp1];
+                else src = &T.int22[typ][t2][a1][sp1][sq1][b1];
+                pfx = *src;
+            }
+        }
+    };
+
+    auto prep = [&](int d) {
+        // item ranges of this wave (estimated cost, x4)
+        const int sq = d - 1;                                   // qm span
+        cp = uni((d <= N - 1) ? L.pcnt[d] : 0);
+        cq = (sq >= 4 && sq <= N - 3) ? N - sq : 0;
+        umax = d - 6 < 30 ? d - 6 : 30;
+        // |S|, |G| of the terms with u <= umax (dev_types.hpp lists, closed form)
+        const int nS = umax < 0 ? 0 : umax <= 5 ? ((umax + 1) * (umax + 2)) / 2 : 21 + 4 * (umax - 5);
+        const int nG = umax < 6 ? 0 : ((umax - 3) * (umax - 2)) / 2 - 3;
+        sS = (nS + WAVE - 1) / WAVE;
+        sG = (nG + WAVE - 1) / WAVE;
+        nit = cq ? (sq - 3 + 15) / 16 : 0;                      // qm: 16 lanes per cell
+        sQ5 = (d - 4 + WAVE - 1) / WAVE;
+        const int cqg = (cq + 3) / 4;                           // qm items = groups of 4 cells
+        const int ca = 4 * sG + 12 * sS + 16, cb = 6 * nit + 12, c5 = 16 * sQ5 + 16;
+        const int Ct = c5 + cp * ca + cqg * cb;
+        const int lo = wid * Ct, hi = lo + Ct;                  // x NW
+        kb_lo = clampi(cdiv_pos(lo - c5 * NW, ca * NW), 0, cp);
+        kb_hi = clampi(cdiv_pos(hi - c5 * NW, ca * NW), 0, cp);
+        const int b2 = c5 + cp * ca;
+        km_lo = 4 * clampi(cdiv_pos(lo - b2 * NW, cb * NW), 0, cqg);
+        km_hi = min(cq, 4 * clampi(cdiv_pos(hi - b2 * NW, cb * NW), 0, cqg));
+        // term descriptors of span d
+        if (d <= 36) {
+#pragma unroll
+            for (int s = 0; s < GSLOTS; s++) {
+                const int t = s * WAVE + lane;
+                const int u = kG[s] - N - 3, n1 = L.gd[t] & 255;
+                const bool ok = t < nG;
+                D.offG[s] = ok ? off(d - 2 - u, N) + n1 : 0;
+                D.fG[s] = ok ? L.gf[t] : 0.f;
+            }
+#pragma unroll
+            for (int s = 0; s < SSLOTS; s++) {
+                const int t = s * WAVE + lane;
+                const int u = kS[s] - N - 3, n1 = int(L.sd[t]) & 255;
+                const bool ok = t < nS;
+                D.offS[s] = ok ? off(d - 2 - u, N) + n1 : 0;
+                D.fS[s] = ok ? L.sf[t] : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < GSLOTS; s++) D.offG[s] += kG[s] - d;
+#pragma unroll
+            for (int s = 0; s < SSLOTS; s++) D.offS[s] += kS[s] - d;
+        }
+        if (kb_lo < kb_hi) load_chunk(d, kb_lo, (kb_hi - kb_lo) < CHUNK ? kb_hi - kb_lo : CHUNK);
+    };
+
 #ifdef ADX_STAMP
     unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
-
-    for (int d = 4; d <= N + 2; ++d) {
+    prep(4);
+    for (int d = 4; d <= N; ++d) {
         STAMP(10);
-        const int buf = d & 1;
-        float *scr = L.scr + buf * NT;
-        const float *pscr = L.scr + (buf ^ 1) * NT;
-        float *scrC = L.scr + 2 * NT;
-        // ---------------- finalize items of the previous iteration
-        const int df = d - 1;                     // qb diagonal to finish
-        const int cdf = (df >= 4 && df <= N - 1) ? N - df : 0;
-        const int dq = d - 3;                     // qm diagonal to finish
-        const int cq = (dq >= 4 && dq <= N - 6) ? N - dq : 0;
-        const int jq = d - 2;                     // q5 index to finish
-        if (tid < cdf) {
-            const int i = tid + 1, j = i + df;
-            const int idx = off(df, N) + i - 1;
-            const int r = pinv(L, df & 3)[i];
-            const int si = L.S[i], sj = L.S[j];
-            const int sim = L.S[i - 1], sjp = L.S[j + 1];
-            const int btype = ptype(si, sj);
-            float qbv = 0.f;
-            if (r != 0xFF) {
-                const int ch = r / WAVE, ln = r % WAVE;
-                for (int sl = 0; sl < p_slA; sl++) qbv += pscr[(sl * p_gA + ch) * WAVE + ln];
-                const int u = df - 1;
-                if (L.up[i + 1] >= u) {
-                    float h = -1.f;
-                    if (u == 3 || u == 4 || u == 6) {
-                        const uint32_t key = hp_key(L.S, i, u + 2);
-                        for (int k = 0; k < nsp; k++)
-                            if (__float_as_uint(L.dt[DT_SPK + k]) == key) { h = L.dt[DT_SPV + k]; break; }
-                    }
-                    if (h < 0.f)
-                        h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + btype]
-                                                        : L.dt[DT_MMH + btype * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
-                    qbv += h;
-                }
-                if (df == mlen - 1 && L.mat[i]) qbv += mextra;
-            }
-            const int code = rtype(btype) * 25 + sjp * 5 + sim;
-            L.qbm[idx] = qbv * L.dt[DT_MMI + code];
-            L.cc[idx] = static_cast<uint8_t>(code);
-            if (df <= N - 6) {
-                float q1 = qbv * L.dt[DT_MLS + btype * 25 + sim * 5 + sjp];
-                if (df >= 5 && L.up[j] >= 1) q1 = fmaf(L.qm1[colb(j - 1) + i - 1], mlbase_sig, q1);
-                L.qm1[colb(j) + i - 1] = q1;
-            }
-        } else if (tid < cdf + cq) {
-            const int r = tid - cdf;
-            const int ch = r / WAVE, ln = r % WAVE;
-            float sq = 0.f;
-            for (int sl = 0; sl < p_slB; sl++) sq += pscr[(p_nA + sl * p_gB + ch) * WAVE + ln];
-            L.qm[rowb(r + 1, N) + dq - 4] = sq;
-        } else if (tid == cdf + cq && jq >= 4 && jq <= N) {
-            L.q5[jq] = ((L.up[jq] >= 1) ? L.q5[jq - 1] * sig1 : 0.f) + scrC[jq & 1];
+        const int sq = d - 1;
+        // ---------------- values iteration d-1 wrote: qm1(i, j-1) and mla(i+1, j-1)
+        // of the first chunk; qm1 of the non-pairable cells of d (stored at the end)
+        float cprev = 0.f, cml = 0.f;
+        if (kb_lo < kb_hi) {
+            const int j = ci + d;
+            cprev = (d >= 5 && L.up[j] >= 1) ? L.qm1[colb(j - 1) + ci - 1] : 0.f;
+            cml = L.mla[((d - 2) & 1) * NP + ci + 1] * cmlc;
         }
-        if (wid == NW - 1 && d + 1 <= N - 1) build_plist(L, N, d + 1, (d + 1) & 3, lane);
+        const int r1 = tid, i1 = r1 + 1, j1 = i1 + d;
+        const bool has1 = r1 < N - d;
+        float m1pre = 1.f, m1prev = 0.f;
+        int m1up = 0;
+        if (has1) {
+            m1pre = L.qm1[colb(j1) + i1 - 1];
+            m1prev = L.qm1[colb(j1 - 1) + i1 - 1];
+            m1up = L.up[j1];
+        }
         STAMP(0);
 
-        // ---------------- jobs
-        const bool jobA = d <= N - 1;
-        const int dbq = d - 2;
-        const bool jobB = dbq >= 4 && dbq <= N - 6;
-        const int cp = jobA ? L.pcount[d & 3] : 0;
-        const int cb = jobB ? N - dbq : 0;
-        const int gA = (cp + WAVE - 1) / WAVE;
-        const int gB = (cb + WAVE - 1) / WAVE;
-        const int umax = d - 6 < 30 ? d - 6 : 30;
-        // job A term list per cell: [7 small shapes | generic (u = 6..umax, n1 = 2..u-2)
-        // | multiloop closing (tp = 6..d-5) | umax bulge pairs | umax-3 1xn pairs]
-        const int nGen = umax >= 6 ? ((umax - 3) * (umax - 2)) / 2 - 3 : 0;
-        const int nML = d > 10 ? d - 10 : 0;
-        const int nBul = umax > 0 ? umax : 0;
-        const int n1n = umax > 3 ? umax - 3 : 0;
-        const int nT = 7 + nGen + nML + nBul + n1n;
-        const int nB = jobB ? dbq - 3 : 0;
-        int nA = 0;
-        if (gA && gB) {
-            const int wA = gA * (6 + nGen + nML + 3 * (nBul + n1n));
-            const int wB = gB * 2 * nB;
-            nA = (NW * wA + (wA + wB) / 2) / (wA + wB);
-            if (nA < gA) nA = gA;
-            if (nA > NW - gB) nA = NW - gB;
-        } else if (gA) {
-            nA = NW;
-        }
-        const int slA = gA ? nA / gA : 0;
-        const int slB = gB ? (NW - nA) / gB : 0;
-
-        if (wid < gA * slA) {
-            // ====================== job A: qb(d) partials
-            const int ch = wid % gA, sl = wid / gA;
-            const int r = ch * WAVE + lane;
-            const bool active = r < cp;
-            const int i = plist(L, d & 3)[active ? r : 0];
-            const int j = i + d;
-            const int type = ptype(L.S[i], L.S[j]);
-            const int si1 = L.S[i + 1], sj1 = L.S[j - 1];
-            const int A_ = L.up[i + 1], B_ = L.dn[j - 1];
-            const int ocode = type * 25 + si1 * 5 + sj1;
-            const float mmI_ij = L.dt[DT_MMI + ocode];
-            const float mlc_ij = L.dt[DT_MLS + rtype(type) * 25 + sj1 * 5 + si1];
-            const bool free_cell = !active || (A_ >= umax && B_ >= umax);
-            const bool masked = constrained && (__ballot(!free_cell) != 0ull);
-            const int t0 = (sl * nT) / slA, t1 = ((sl + 1) * nT) / slA;
-            const float tau_ij = type > 2 ? eTAU : 1.f;
-            // ---- small shapes: int11/21/22 come from HBM/L2, so they are issued
-            // first and consumed after the LDS-bound loops
-            float smq[7], smf[7];
-#pragma unroll
-            for (int s = 0; s < 7; s++) {
-                smq[s] = 0.f;
-                smf[s] = 0.f;
-                const int n1 = (s == 0) ? 0 : (s == 1 || s == 2) ? 1 : (s == 6) ? 3 : 2;
-                const int n2 = (s == 0) ? 0 : (s == 1 || s == 3) ? 1 : (s == 2 || s == 4 || s == 6) ? 2 : 3;
-                const int u = n1 + n2;
-                if (s >= t0 && s < t1 && u <= umax) {
-                    const int ix = off(d - 2 - u, N) + i + n1;
-                    const int code = L.cc[ix];
-                    const int t2 = (code * 41) >> 10;
-                    const int p = i + 1 + n1, q = j - 1 - n2;
-                    const int sp1 = L.S[p - 1], sq1 = L.S[q + 1];
-                    const bool ok = !masked || ((n1 <= A_) & (n2 <= B_));
-                    smq[s] = ok ? L.qbm[ix] * ct[CT_INVMM + code] : 0.f;
-                    if (s == 0) smf[s] = ct[CT_STK + type * 8 + t2] * ct[CT_FSM + 0];
-                    else if (s == 1) smf[s] = T.int11[type][t2][si1][sj1] * ct[CT_FSM + 2];
-                    else if (s == 2) smf[s] = T.int21[type][t2][si1][sq1][sj1] * ct[CT_FSM + 3];
-                    else if (s == 3) smf[s] = T.int21[t2][type][sq1][si1][sp1] * ct[CT_FSM + 3];
-                    else if (s == 4) smf[s] = T.int22[type][t2][si1][sp1][sq1][sj1] * ct[CT_FSM + 4];
-                    else smf[s] = ct[CT_M23O + ocode] * ct[CT_M23O + code] * ct[CT_FSM + 5];
-                }
-            }
-            STAMP(1);
-            float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#ifndef ADX_ABL_GENERIC
-            // ---- generic interior loops: contiguous n1 runs of one u per row
-            {
-                const int gs = (t0 > 7 ? t0 : 7) - 7, ge = (t1 < 7 + nGen ? t1 : 7 + nGen) - 7;
-                if (gs < ge) {
-                    int u = 6, rs = 0;
-                    while (rs + (u - 3) <= gs) { rs += u - 3; u++; }
-                    int idx = gs;
-                    while (idx < ge) {
-                        const int a = 2 + (idx - rs);
-                        const int rowend = rs + (u - 3);
-                        const int e = (ge < rowend ? ge : rowend) - rs + 2;  // n1 in [a, e)
-                        const float *fr = XS->fgen + (u - 6) * FG_ROW - 2;    // fr[n1] (scalar loads)
-                        const float *q = L.qbm + off(d - 2 - u, N) + i;  // q[n1] = qbm(i+1+n1, j-1-u+n1)
-                        int n1 = a;
-                        if (!masked) {
-                            for (; n1 + 8 <= e; n1 += 8) {
-                                float qv[8], fv[8];
-#pragma unroll
-                                for (int k = 0; k < 8; k++) { qv[k] = q[n1 + k]; fv[k] = fr[n1 + k]; }
-#pragma unroll
-                                for (int k = 0; k < 8; k++) g[k] = fmaf(qv[k], fv[k], g[k]);
-                            }
-                            for (; n1 + 2 <= e; n1 += 2) {
-                                const float q0 = q[n1], q1 = q[n1 + 1];
-                                g[0] = fmaf(q0, fr[n1], g[0]);
-                                g[1] = fmaf(q1, fr[n1 + 1], g[1]);
-                            }
-                            if (n1 < e) g[2] = fmaf(q[n1], fr[n1], g[2]);
-                        } else {
-                            const int lo = u - B_;  // n2 <= B_  <=>  n1 >= u - B_
-                            for (; n1 + 4 <= e; n1 += 4) {
-                                float qv[4];
-#pragma unroll
-                                for (int k = 0; k < 4; k++) qv[k] = q[n1 + k];
-#pragma unroll
-                                for (int k = 0; k < 4; k++) {
-                                    const bool ok = (n1 + k <= A_) & (n1 + k >= lo);
-                                    g[k] = fmaf(qv[k], ok ? fr[n1 + k] : 0.f, g[k]);
-                                }
-                            }
-                            for (; n1 < e; n1++) {
-                                const bool ok = (n1 <= A_) & (n1 >= lo);
-                                g[4] = fmaf(q[n1], ok ? fr[n1] : 0.f, g[4]);
-                            }
-                        }
-                        idx = rs + (e - 2);
-                        rs = rowend;
-                        u++;
-                    }
-                }
-            }
-#endif
-            STAMP(2);
-            float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#ifndef ADX_ABL_ML
-            // ---- multiloop closed by (i,j): qm[i+1][k-1] * qm1[k][j-1], k = i + tp
-            {
-                const int b0 = 7 + nGen;
-                const int ms = (t0 > b0 ? t0 : b0) - b0, me = (t1 < b0 + nML ? t1 : b0 + nML) - b0;
-                if (ms < me) {
-                    const float *qa = L.qm + rowb(i + 1, N);          // qa[m] = qm[i+1][i+tp-1], tp = 6 + m
-                    const float *qb1 = L.qm1 + colb(j - 1) + i + 5;   // qb1[m] = qm1[i+tp][j-1]
-                    int mm = ms;
-                    for (; mm + 8 <= me; mm += 8) {
-                        float av[8], bv[8];
-#pragma unroll
-                        for (int k = 0; k < 8; k++) { av[k] = qa[mm + k]; bv[k] = qb1[mm + k]; }
-#pragma unroll
-                        for (int k = 0; k < 8; k++) m[k] = fmaf(av[k], bv[k], m[k]);
-                    }
-                    for (; mm < me; mm++) m[0] = fmaf(qa[mm], qb1[mm], m[0]);
-                }
-            }
-#endif
-            STAMP(3);
-            float sA = 0.f, sB = 0.f, sC = 0.f, sD = 0.f;
-#ifndef ADX_ABL_SPECIAL
-            {
-                const int b0 = 7 + nGen + nML;
-                // bulges (0,n) and (n,0), n = 1..umax: unit n - 1 covers both sides
-                {
-                    const int bs = (t0 > b0 ? t0 : b0) - b0;
-                    const int be = (t1 < b0 + nBul ? t1 : b0 + nBul) - b0;
-                    int n = bs + 1;
-                    int o = off(d - 2 - n, N) + i;  // cell (i+1, j-1-n)
-                    if (n == 1 && n <= be) {
-                        const int c0 = L.cc[o], c1 = L.cc[o + 1];
-                        const float v0 = L.qbm[o], v1 = L.qbm[o + 1];
-                        const float f0 = ct[CT_FSM + 1];
-                        const float x0 = ct[CT_INVMM + c0] * ct[CT_STK + type * 8 + ((c0 * 41) >> 10)] * f0;
-                        const float x1 = ct[CT_INVMM + c1] * ct[CT_STK + type * 8 + ((c1 * 41) >> 10)] * f0;
-                        const bool ok0 = !masked || (1 <= B_), ok1 = !masked || (1 <= A_);
-                        sA = fmaf(v0, ok0 ? x0 : 0.f, sA);
-                        sB = fmaf(v1, ok1 ? x1 : 0.f, sB);
-                        o -= N - (d - 4);  // off(D-1) = off(D) - (N - D + 1), D = d-3
-                        n++;
-                    }
-                    // two units per iteration: 4 independent cc/qbm loads in flight
-                    for (; n + 1 <= be; n += 2) {
-                        const int o2 = o - (N - (d - 3 - n));
-                        const int c0 = L.cc[o], c1 = L.cc[o + n], c2 = L.cc[o2], c3 = L.cc[o2 + n + 1];
-                        const float v0 = L.qbm[o], v1 = L.qbm[o + n], v2 = L.qbm[o2], v3 = L.qbm[o2 + n + 1];
-                        const float fb0 = XS->ctab[CT_FB + n] * tau_ij, fb1 = XS->ctab[CT_FB + n + 1] * tau_ij;
-                        const float x0 = ct[CT_BUL + c0] * fb0, x1 = ct[CT_BUL + c1] * fb0;
-                        const float x2 = ct[CT_BUL + c2] * fb1, x3 = ct[CT_BUL + c3] * fb1;
-                        const bool ok0 = !masked || (n <= B_), ok1 = !masked || (n <= A_);
-                        const bool ok2 = !masked || (n + 1 <= B_), ok3 = !masked || (n + 1 <= A_);
-                        sA = fmaf(v0, ok0 ? x0 : 0.f, sA);
-                        sB = fmaf(v1, ok1 ? x1 : 0.f, sB);
-                        sC = fmaf(v2, ok2 ? x2 : 0.f, sC);
-                        sD = fmaf(v3, ok3 ? x3 : 0.f, sD);
-                        o = o2 - (N - (d - 4 - n));
-                    }
-                    if (n <= be) {
-                        const int c0 = L.cc[o], c1 = L.cc[o + n];
-                        const float fb = ct[CT_FB + n] * tau_ij;
-                        const bool ok0 = !masked || (n <= B_), ok1 = !masked || (n <= A_);
-                        sA = fmaf(L.qbm[o], ok0 ? ct[CT_BUL + c0] * fb : 0.f, sA);
-                        sB = fmaf(L.qbm[o + n], ok1 ? ct[CT_BUL + c1] * fb : 0.f, sB);
-                    }
-                }
-                // 1 x nl and nl x 1, nl = 3..umax-1: unit nl - 3 covers both sides
-                {
-                    const int s0 = b0 + nBul;
-                    const int bs = (t0 > s0 ? t0 : s0) - s0, be = t1 - s0;
-                    if (bs < be) {
-                        const float mo = ct[CT_ONEN + ocode] * mmI_ij;  // outer mismatch_1n
-                        int nl = bs + 3;
-                        const int nle = be + 3;
-                        int o = off(d - 3 - nl, N) + i;  // cell (i+2, j-1-nl) at o + 1
-                        for (; nl + 1 < nle; nl += 2) {
-                            const int o2 = o - (N - (d - 4 - nl));
-                            const int c0 = L.cc[o + 1], c1 = L.cc[o + nl], c2 = L.cc[o2 + 1], c3 = L.cc[o2 + nl + 1];
-                            const float v0 = L.qbm[o + 1], v1 = L.qbm[o + nl];
-                            const float v2 = L.qbm[o2 + 1], v3 = L.qbm[o2 + nl + 1];
-                            const float f0 = XS->ctab[CT_F1N + nl] * mo, f1 = XS->ctab[CT_F1N + nl + 1] * mo;
-                            const bool ok0 = !masked || ((1 <= A_) & (nl <= B_));
-                            const bool ok1 = !masked || ((nl <= A_) & (1 <= B_));
-                            const bool ok2 = !masked || ((1 <= A_) & (nl + 1 <= B_));
-                            const bool ok3 = !masked || ((nl + 1 <= A_) & (1 <= B_));
-                            sA = fmaf(v0, ok0 ? ct[CT_ONEN + c0] * f0 : 0.f, sA);
-                            sB = fmaf(v1, ok1 ? ct[CT_ONEN + c1] * f0 : 0.f, sB);
-                            sC = fmaf(v2, ok2 ? ct[CT_ONEN + c2] * f1 : 0.f, sC);
-                            sD = fmaf(v3, ok3 ? ct[CT_ONEN + c3] * f1 : 0.f, sD);
-                            o = o2 - (N - (d - 5 - nl));
-                        }
-                        if (nl < nle) {
-                            const int c0 = L.cc[o + 1], c1 = L.cc[o + nl];
-                            const float f0 = ct[CT_F1N + nl] * mo;
-                            const bool ok0 = !masked || ((1 <= A_) & (nl <= B_));
-                            const bool ok1 = !masked || ((nl <= A_) & (1 <= B_));
-                            sA = fmaf(L.qbm[o + 1], ok0 ? ct[CT_ONEN + c0] * f0 : 0.f, sA);
-                            sB = fmaf(L.qbm[o + nl], ok1 ? ct[CT_ONEN + c1] * f0 : 0.f, sB);
-                        }
-                    }
-                }
-            }
-#endif
-            float sm = 0.f;
-#pragma unroll
-            for (int s = 0; s < 7; s++) sm = fmaf(smq[s], smf[s], sm);
-            const float gsum = ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
-            const float msum = ((m[0] + m[1]) + (m[2] + m[3])) + ((m[4] + m[5]) + (m[6] + m[7]));
-            const float part = ((sA + sB) + (sC + sD)) + sm + gsum * mmI_ij + msum * (mlclosing * mlc_ij);
-            scr[wid * WAVE + lane] = part;
-            STAMP(4);
-        } else if (wid >= nA && wid < nA + gB * slB) {
-            // ====================== job B: qm(dbq) partials
-            // qm[i][jb] = sum_t (pre(t) + qm[i][i+t-1]) * qm1[i+t][jb]
-            const int lw = wid - nA;
-            const int ch = lw % gB, sl = lw / gB;
-            const int r = ch * WAVE + lane;
-            const bool active = r < cb;
-            const int i = (active ? r : 0) + 1;
-            const int jb = i + dbq;
-            const int upi = L.up[i];
-            const int t0 = (sl * nB) / slB, t1 = ((sl + 1) * nB) / slB;
-            const float *q1 = L.qm1 + colb(jb) + i - 1;   // q1[t] = qm1[i+t][jb]
-            const float *qr = L.qm + rowb(i, N) - 5;      // qr[t] = qm[i][i+t-1], t >= 5
-            float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            int t = t0;
-            for (; t < t1 && t < 5; t++) a[0] = fmaf((t <= upi) ? XS->pwml[t] : 0.f, q1[t], a[0]);
-            if (!constrained) {
-                for (; t + 8 <= t1; t += 8) {
-                    float pv[8], rv[8], qv[8];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) { pv[k] = XS->pwml[t + k]; rv[k] = qr[t + k]; qv[k] = q1[t + k]; }
-#pragma unroll
-                    for (int k = 0; k < 8; k++) a[k] = fmaf(pv[k] + rv[k], qv[k], a[k]);
-                }
-            }
-            for (; t < t1; t++) a[1] = fmaf(((t <= upi) ? XS->pwml[t] : 0.f) + qr[t], q1[t], a[1]);
-            scr[wid * WAVE + lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-            STAMP(5);
-        }
-        if (wid == NW - 1 && d - 1 >= 4 && d - 1 <= N) {
-            // ====================== job C: q5[j] partial, j = d-1
-            const int j = d - 1;
-            float extf[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int k = 1 + lane + c * WAVE;
-                extf[c] = 0.f;
-                if (k <= j - 4) {
-                    const int type = ptype(L.S[k], L.S[j]);
-                    extf[c] = L.dt[DT_EXT + type * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + ((j < N) ? L.S[j + 1] : 5)];
-                }
-            }
+        // ---------------- q5[d] (wave 0)
+        if (wid == 0) {
+            const int j = d;
+            const int sjp = (j < N) ? L.S[j + 1] : 5;
+            const int sj = L.S[j];
             float acc = 0.f;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int k = 1 + lane + c * WAVE;
-                if (k <= j - 4) {
-                    const int ix = off(j - k, N) + k - 1;
-                    acc = fmaf(L.q5[k - 1] * L.qbm[ix], ct[CT_INVMM + L.cc[ix]] * extf[c], acc);
+            for (int q = 0; q < sQ5; q++) {
+                const int k0 = q * WAVE + lane + 1;
+                const bool ok = k0 <= j - 4;
+                const int k = ok ? k0 : 1;
+                const int ix = off(j - k, N) + k - 1;
+                const int ty = ptype(L.S[k], sj);
+                const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + sjp];
+                const float x = L.q5[k - 1] * L.qbm[ix];
+                acc = fmaf(x, ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f, acc);
+            }
+            const float sum = wave_sum(acc);
+            if (lane == 0) L.q5[j] = ((L.up[j] >= 1) ? L.q5[j - 1] * sig1 : 0.f) + sum;
+        }
+        STAMP(6);
+
+        // ---------------- qm(i, i+sq) and mla(i, sq), groups of 4 cells,
+        // 16 lanes (split points t = it*16 + l16) per cell:
+        // qm[i][jb] = sum_t (pw(t) + qm[i][i+t-1]) * qm1[i+t][jb]
+        {
+            const int g = lane >> 4, l16 = lane & 15;
+            const int tmax = sq - 4;
+            for (int m0 = km_lo; m0 < km_hi; m0 += 4) {
+                const int m = m0 + g;
+                const bool cell = m < km_hi;
+                const int i = m + 1, jb = i + sq;
+                const int upi = constrained ? L.up[cell ? i : 1] : 255;
+                const float *q1 = L.qm1 + colb(jb) + i - 1;
+                const float *qr = L.qm + rowb(i, N) - 5;
+                float A0 = 0.f, P0 = 0.f, A1 = 0.f, P1 = 0.f;
+                int it = 0;
+                for (; it + 2 <= nit; it += 2) {
+                    const int t0 = it * 16 + l16, t1 = t0 + 16;
+                    const bool ok0 = cell && t0 <= tmax, ok1 = cell && t1 <= tmax;
+                    const float v0 = q1[ok0 ? t0 : 0], v1 = q1[ok1 ? t1 : 0];
+                    const float r0 = qr[(ok0 && t0 >= 5) ? t0 : 5], r1v = qr[(ok1 && t1 >= 5) ? t1 : 5];
+                    const float w0 = L.pw[t0 <= N ? t0 : N], w1 = L.pw[t1 <= N ? t1 : N];
+                    const float b0 = ok0 ? v0 : 0.f, b1 = ok1 ? v1 : 0.f;
+                    A0 = fmaf((ok0 && t0 >= 5) ? r0 : 0.f, b0, A0);
+                    A1 = fmaf((ok1 && t1 >= 5) ? r1v : 0.f, b1, A1);
+                    P0 = fmaf((t0 <= upi) ? w0 : 0.f, b0, P0);
+                    P1 = fmaf((t1 <= upi) ? w1 : 0.f, b1, P1);
+                }
+                if (it < nit) {
+                    const int t0 = it * 16 + l16;
+                    const bool ok0 = cell && t0 <= tmax;
+                    const float v0 = q1[ok0 ? t0 : 0];
+                    const float r0 = qr[(ok0 && t0 >= 5) ? t0 : 5];
+                    const float w0 = L.pw[t0 <= N ? t0 : N];
+                    const float b0 = ok0 ? v0 : 0.f;
+                    A0 = fmaf((ok0 && t0 >= 5) ? r0 : 0.f, b0, A0);
+                    P0 = fmaf((t0 <= upi) ? w0 : 0.f, b0, P0);
+                }
+                const float sA = row_sum(A0 + A1);
+                const float sP = row_sum(P0 + P1);
+                if (l16 == 15 && cell) {
+                    L.qm[rowb(i, N) + sq - 4] = sA + sP;
+                    L.mla[(sq & 1) * NP + i] = sA;
                 }
             }
-            acc = wave_sum(acc);
-            if (lane == 0) scrC[j & 1] = acc;
-            STAMP(6);
         }
-        p_gA = gA;
-        p_slA = slA;
-        p_gB = gB;
-        p_slB = slB;
-        p_nA = nA;
-        STAMP(8);
+        STAMP(5);
+
+        // ---------------- qb(i, i+d): lanes = interior-loop terms
+        for (int kc = kb_lo; kc < kb_hi; kc += CHUNK) {
+            const int nc = (kb_hi - kc) < CHUNK ? kb_hi - kc : CHUNK;
+            if (kc != kb_lo) {
+                load_chunk(d, kc, nc);
+                const int j = ci + d;
+                cprev = (d >= 5 && L.up[j] >= 1) ? L.qm1[colb(j - 1) + ci - 1] : 0.f;
+                cml = L.mla[((d - 2) & 1) * NP + ci + 1] * cmlc;
+            }
+            float sums = 0.f;
+            for (int c = 0; c < nc; c++) {
+                CellU u;
+                u.i = __builtin_amdgcn_readlane(ci, c);
+                u.ty8 = __builtin_amdgcn_readlane(cty, c) * 8;
+                u.A = __builtin_amdgcn_readlane(cA, c);
+                u.B = __builtin_amdgcn_readlane(cB, c);
+                u.mmo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cmmo), c));
+                u.tau = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ctau), c));
+                u.mo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cmo), c));
+                u.m23 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cm23), c));
+                const bool masked = constrained && (u.A < umax || u.B < umax);
+                // gather of the prefetched 1x1..2x2 table factors for this cell
+                const float gtab = __shfl(pfx, c * 4 + D.gsel, WAVE);
+                const float part = masked ? qb_terms_dispatch<true>(sS, sG, L, D, u, gtab)
+                                          : qb_terms_dispatch<false>(sS, sG, L, D, u, gtab);
+                const float tot = wave_sum(part);
+                sums = (lane == c) ? tot : sums;
+            }
+            if (lane < nc) {
+                const float qb = sums + cpre + cml;
+                L.qbm[cidx] = qb * cmmc + 0.0f;   // never -0 (the non-pairable mark)
+                L.qm1[cm1] = fmaf(qb, cpm1, cprev * mlbase_sig);
+            }
+        }
+        if (has1 && m1pre == 0.f) L.qm1[colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? m1prev * mlbase_sig : 0.f;
+        STAMP(4);
+        if (d < N) prep(d + 1);
+        STAMP(7);
         __syncthreads();
         STAMP(9);
     }
@@ -678,9 +775,7 @@ __device__ double pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Ld
     if (lane == 0 && wid < 16)
         for (int k = 0; k < 12; k++) atomicAdd(&g_stamps[wid][k], st_acc[k]);
 #endif
-    const float z = L.q5[N];
-    const double lnZ = log(static_cast<double>(z)) - N * X.log_sigma;
-    return -X.kT * lnZ;
+    return L.q5[N];   // scaled Z; the energy is taken after the variant loop
 }
 
 // ---------------------------------------------------------------- scoring
@@ -709,15 +804,21 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
                                  const uint8_t *raw, const Lds &L,
                                  float *dG_out, double *terms_out) {
     for (int v = 0; v < ka.n_variants; v++) {
-        const double g = pf_inside<NT>(ka, v, raw, L, XS);
-        if (threadIdx.x == 0) {
+        const float z = pf_inside<NT>(ka, v, raw, L, XS);
+        if (threadIdx.x == 0) L.G[v] = static_cast<double>(z);
+        __syncthreads();   // the next variant rewrites the tables
+    }
+    double s = 0.0;
+    if (threadIdx.x == 0) {
+        // ensemble energy -kT (ln Z_scaled - N ln sigma), as vrna_pf (float)
+        for (int v = 0; v < ka.n_variants; v++) {
+            const int N = ka.variants[v].N;
+            const double g = -XS->kT * (log(L.G[v]) - N * XS->log_sigma);
             L.G[v] = g;
             if (dG_out) dG_out[v] = static_cast<float>(g);
         }
+        s = combine_score(ka, L, terms_out);
     }
-    __syncthreads();
-    double s = 0.0;
-    if (threadIdx.x == 0) s = combine_score(ka, L, terms_out);
     return s;
 }
 
@@ -726,11 +827,12 @@ __global__ void __launch_bounds__(NT, 4)
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Lds L = carve<NT>(smem, ka);
+    Lds L;
+    lds_layout<false>(smem, ka.cells, ka.Nmax, ka.n_variants, &L);
     const int w = blockIdx.x;
     if (w >= W) return;
     if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
-    load_ctab<NT>(ka, L);
+    load_ctab(ka, L);
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
@@ -949,12 +1051,8 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 }  // namespace
 
 // ---------------------------------------------------------------- host launchers
-size_t lds_bytes(const KArgs &ka, bool /*unused*/, int nt) {
-    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-    const size_t C = size_t(ka.cells);
-    const size_t NP = size_t(ka.Nmax) + 2;
-    return 3 * al(C * 4) + al(C) + al(2 * nt * 4 + 16) + al(CT_SIZE * 4) + al(size_t(896 + 2 * MAX_SPECIAL_HP + ka.Nmax + 1) * 4) + al(NP * 4) + al(16 * 4) +
-           al(size_t(ka.n_variants) * 8) + al(16) + 8 * al(NP) + al(8 * NP);
+size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
+    return lds_layout<true>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr);
 }
 
 constexpr int NT_DEFAULT = 512;

@@ -18,8 +18,10 @@ L.adx_debug_stamps(buf, 1)
 eng.score_batch([tmpl])
 L.adx_debug_stamps(buf, 1)
 V = eng.info.n_variants
-names = ["prefetch", "smallA", "generic", "ML", "special", "jobB", "jobC", "bar1", "phaseB", "bar2", "looptop"]
+# stamp ids (kernels.hip STAMP(k)): 10 loop top + qm1 pass, 0 descriptors + chunk 0,
+# 6 q5, 5 qm items, 4 qb cells + finalize, 9 barrier
+cols = [(10, "top"), (0, "late"), (6, "q5"), (5, "qm"), (4, "qb"), (7, "prep"), (9, "barrier")]
 print("cycles per PF per wave (avg over %d variants)" % V)
-print("wave " + " ".join("%9s" % n for n in names))
+print("wave " + " ".join("%9s" % n for _, n in cols))
 for w in range(8):
-    print("%4d " % w + " ".join("%9d" % (buf[w * 16 + k] // V) for k in range(11)))
+    print("%4d " % w + " ".join("%9d" % (buf[w * 16 + k] // V) for k, _ in cols))
