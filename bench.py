@@ -84,7 +84,7 @@ def main():
         dist_.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = dist_
 
-    from addapt_amd import native, roofline, workloads
+    from addapt_amd import native, roofline, shard, workloads
 
     tmpl, active = workloads.synthetic(a.length)
     terms = workloads.default_objective()
@@ -92,8 +92,8 @@ def main():
     th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank)
     W = a.walkers
-    gids = [rank * W + w for w in range(W)]
-    seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + rank * W)
+    gids = shard.walker_ids(rank, world, W)
+    seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + gids[0])
     eng.walkers_init(gids, seqs)
 
     def barrier():
@@ -113,19 +113,14 @@ def main():
     t1 = time.perf_counter()
     kernel_ms = eng.last_kernel_ms()
     _, _, c1 = eng.download()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(t1 - t0, dist, device="cuda" if dist is not None else None)
     steps_total = W * a.steps * world
     value = steps_total / elapsed
 
     # algorithmic FLOPs of the launch: scored steps x sum over the PF variants
     dc = c1 - c0
     scored = int(dc[:, 0].sum() + dc[:, 1].sum() + dc[:, 3].sum())
+    outcomes = shard.sum_over_ranks(dc.sum(axis=0), dist, device="cuda" if dist is not None else None)
     sample = [tmpl] + seqs[:7]
     f_free = sum(roofline.pf_flops(s, None) for s in sample) / len(sample)
     f_act = sum(roofline.pf_flops(s, active) for s in sample) / len(sample)
@@ -174,7 +169,7 @@ def main():
             "global_walkers": W * world,
             "length": a.length,
             "parallelism": "walker-sharded x%d (no data-path collective)" % world,
-            "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, dc.sum(axis=0))},
+            "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, outcomes)},
         },
         "roofline": roof,
     }
