@@ -49,7 +49,7 @@ def test_walker_sequences(oracle):
             assert dict(A="U", U="A", G="C", C="G")[s[k]] == s[99 - k]
 
 
-@pytest.mark.parametrize("N", [55, 70])
+@pytest.mark.parametrize("N", [60, 72])
 def test_roofline_term_counts_match_oracle(oracle, N):
     tmpl, act = workloads.synthetic(N)
     for cst in (None, act):
