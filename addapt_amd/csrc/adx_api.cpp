@@ -24,7 +24,7 @@ namespace adx {
 size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
 hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
                         double *terms, float *dG, hipStream_t stream);
-hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream);
+hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream, hipEvent_t *evs);
 constexpr int NT = 512;
 constexpr size_t LDS_MAX = 163840;
 }  // namespace adx
@@ -627,6 +627,8 @@ struct adx_ctx {
     DevBuf<uint8_t> d_clo_par;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
+    double score_ms_total = 0.0;   // sum of the score-kernel launch durations of the last run
+    int score_launches = 0;
 
     ~adx_ctx() {
         if (ev0) (void)hipEventDestroy(ev0);
@@ -966,13 +968,28 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
         st.tr_u = tu.p;
         st.tr_terms = ntt > 0 ? tterms.p : nullptr;
     }
+    // events around every score launch (the dominant kernel) for its average duration
+    std::vector<hipEvent_t> evs(2 * size_t(steps));
+    for (auto &e : evs) HIP_TRY(hipEventCreate(&e));
+    struct EvFree {
+        std::vector<hipEvent_t> &v;
+        ~EvFree() { for (auto e : v) (void)hipEventDestroy(e); }
+    } evfree{evs};
     HIP_TRY(hipEventRecord(c->ev0, pb.stream));
-    HIP_TRY(launch_steps(pb.kargs(), pb.qbm, st, pb.stream));
+    HIP_TRY(launch_steps(pb.kargs(), pb.qbm, st, pb.stream, evs.data()));
     HIP_TRY(hipEventRecord(c->ev1, pb.stream));
     HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last_ms = ms;
+    double sk = 0.0;
+    for (int k = 0; k < steps; k++) {
+        float e = 0.f;
+        HIP_TRY(hipEventElapsedTime(&e, evs[2 * k], evs[2 * k + 1]));
+        sk += e;
+    }
+    c->score_ms_total = sk;
+    c->score_launches = steps;
     c->step += steps;
     std::vector<int> errs(W);
     HIP_TRY(hipMemcpy(errs.data(), c->err.p, sizeof(int) * W, hipMemcpyDeviceToHost));
@@ -999,6 +1016,13 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
 extern "C" adx_status adx_last_kernel_ms(const adx_ctx *c, double *ms) {
     if (!c || !ms) return fail(ADX_EINVAL, "adx_last_kernel_ms: null argument");
     *ms = c->last_ms;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_last_score_kernel_ms(const adx_ctx *c, double *avg_ms, int *launches) {
+    if (!c || !avg_ms) return fail(ADX_EINVAL, "adx_last_score_kernel_ms: null argument");
+    *avg_ms = c->score_launches ? c->score_ms_total / c->score_launches : 0.0;
+    if (launches) *launches = c->score_launches;
     return ADX_OK;
 }
 

@@ -1077,12 +1077,15 @@ hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, doubl
     return launch_score_m(ka, seqs, W, scores, terms, dG, nullptr, stream);
 }
 
-hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream) {
+// evs (optional): 2 * nsteps events recorded around each step's score launch
+hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
     for (int s = 0; s < st.nsteps; s++) {
         hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
+        if (evs) (void)hipEventRecord(evs[2 * s], stream);
         hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
+        if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot);
     }

@@ -69,7 +69,7 @@ EXPORTS = [
     "adx_last_error", "adx_abi_version", "adx_params_load", "adx_params_free", "adx_kT",
     "adx_eval_structure", "adx_fold_create", "adx_fold_add_motif", "adx_fold_add_constraint",
     "adx_fold_pf", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
-    "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms",
+    "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc",
 ]
 
@@ -101,6 +101,7 @@ def lib():
         L.adx_walkers_init.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_uint32)]
         L.adx_run_steps.argtypes = [C.c_void_p, C.c_int, C.POINTER(Trace)]
         L.adx_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.adx_last_score_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.adx_walkers_download.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
                                            C.POINTER(C.c_int64)]
         L.adx_score_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_double),
@@ -293,6 +294,12 @@ class Engine:
         ms = C.c_double()
         _check(lib().adx_last_kernel_ms(self.ptr, C.byref(ms)))
         return ms.value
+
+    def last_score_kernel_ms(self):
+        """(average score-kernel launch ms, launches) of the last run_steps."""
+        ms, n = C.c_double(), C.c_int()
+        _check(lib().adx_last_score_kernel_ms(self.ptr, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
 
     def download(self):
         W = self.W

@@ -38,8 +38,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="approximate budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (tools/pmc_traffic.py) to fill roofline.traffic")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic")
     return ap.parse_args()
 
 
@@ -111,7 +111,8 @@ def main():
     eng.run_steps(a.steps)
     barrier()
     t1 = time.perf_counter()
-    kernel_ms = eng.last_kernel_ms()
+    kernel_ms = eng.last_kernel_ms()            # whole timed run_steps (3 kernels per step)
+    score_ms, launches = eng.last_score_kernel_ms()   # dominant kernel, per launch
     _, _, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device="cuda" if dist is not None else None)
     steps_total = W * a.steps * world
@@ -125,12 +126,14 @@ def main():
     f_free = sum(roofline.pf_flops(s, None) for s in sample) / len(sample)
     f_act = sum(roofline.pf_flops(s, active) for s in sample) / len(sample)
     flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
-    launch_flops = scored * flop_per_scored
-    achieved_tflops = launch_flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else None
-    traffic = None
+    launch_flops = scored * flop_per_scored / max(1, launches)      # per score launch
+    achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
+    traffic, traffic_src = None, None
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
-            traffic = json.load(f).get("bytes_per_launch")
+            tj = json.load(f)
+        traffic = tj.get("bytes_per_launch")
+        traffic_src = os.path.relpath(a.traffic_json, ROOT)
     roof = {
         "bound": "mfma",
         "achieved": achieved_tflops,
@@ -140,12 +143,17 @@ def main():
         "traffic": traffic,
         "compute_unit": "fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
                         "products, not a contraction); peak = gfx950 fp32 rate, vector == matrix",
-        "kernel": "step_kernel<512,qbm>",
-        "kernel_ms_per_launch": kernel_ms,
+        "kernel": "score_kernel<512>",
+        "traffic_source": traffic_src,
+        "kernel_ms_per_launch": score_ms,
+        "launches": launches,
+        "all_kernels_ms_per_step": kernel_ms / a.steps,
         "flop_per_scored_step": flop_per_scored,
-        "scored_steps_in_launch": scored,
-        "hbm_algorithmic_GBps": (scored * (4 * 100 + 8) + W * a.steps * 16) / (kernel_ms * 1e-3) / 1e9
-        if kernel_ms > 0 else None,
+        "flop_per_launch": launch_flops,
+        "scored_walkers_per_launch": scored / max(1, launches),
+        # compulsory HBM bytes of one launch: each scored walker reads its
+        # proposal (N B) and writes its score (8 B)
+        "algorithmic_bytes_per_launch": (scored / max(1, launches)) * (a.length + 8),
     }
     out = {
         "metric": METRIC,

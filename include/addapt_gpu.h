@@ -173,6 +173,10 @@ adx_status adx_run_steps(adx_ctx *ctx, int steps, adx_trace *trace);
 /* Device time (ms) of the last adx_run_steps / adx_score_batch, measured with
  * HIP events on the context's stream. */
 adx_status adx_last_kernel_ms(const adx_ctx *ctx, double *ms);
+/* Average duration of the score kernel (the fold -> score launch, the dominant
+ * kernel) over the launches of the last adx_run_steps, from HIP events recorded
+ * on the context's stream around each launch. */
+adx_status adx_last_score_kernel_ms(const adx_ctx *ctx, double *avg_ms, int *launches);
 
 adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
 
