@@ -359,6 +359,8 @@ struct Problem {
     std::vector<int> motif_pt;
     double g0 = -0.30;  // assumed free energy per nucleotide for the pf scale
     std::vector<DevVariant> variants;
+    std::vector<int> vmac;       // per variant: macrostate index, -1 = unconstrained
+    std::vector<int> groups2;    // variant pairs folded in lockstep (kernels.hip pf_group)
     std::vector<uint8_t> cons;
     std::vector<uint8_t> ctx_seq;
     std::vector<int> ctx_off;
@@ -371,6 +373,7 @@ struct Problem {
     DevBuf<uint8_t> dCons, dCtxSeq;
     DevBuf<int> dCtxOff;
     DevBuf<DevTermMap> dTmap;
+    DevBuf<int> dGroups2;
     std::unique_ptr<DevTables> hT;
     std::unique_ptr<DevScaled> hX;
 
@@ -409,6 +412,8 @@ struct Problem {
         ka.Nraw = Nraw;
         ka.Nmax = Nmax;
         ka.cells = Nmax >= 5 ? (Nmax - 4) * (Nmax - 3) / 2 : 1;
+        ka.groups2 = dGroups2.p;
+        ka.n_groups2 = static_cast<int>(groups2.size() / 2);
         return ka;
     }
 
@@ -444,6 +449,26 @@ struct Problem {
         HIP_TRY(dCtxSeq.upload(ctx_seq.data(), ctx_seq.size(), stream));
         HIP_TRY(dCtxOff.upload(ctx_off.data(), ctx_off.size(), stream));
         HIP_TRY(dTmap.upload(tmap.data(), tmap.size(), stream));
+        // apo / holo variants of one (context, macrostate) share every cell: pair them
+        groups2.clear();
+        if (vmac.size() != variants.size()) vmac.assign(variants.size(), -1);
+        std::vector<char> used(variants.size(), 0);
+        for (size_t v = 0; v < variants.size(); v++) {
+            if (used[v]) continue;
+            used[v] = 1;
+            size_t mate = v;
+            for (size_t w = v + 1; w < variants.size(); w++) {
+                if (!used[w] && variants[w].ctx == variants[v].ctx && vmac[w] == vmac[v] &&
+                    variants[w].N == variants[v].N && variants[w].motif != variants[v].motif) {
+                    mate = w;
+                    used[w] = 1;
+                    break;
+                }
+            }
+            groups2.push_back(static_cast<int>(v));
+            groups2.push_back(static_cast<int>(mate));
+        }
+        HIP_TRY(dGroups2.upload(groups2.data(), groups2.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
         return choose_layout();
     }
@@ -775,6 +800,7 @@ extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
         pb.cons.insert(pb.cons.end(), blob.begin(), blob.end());
         const int id = static_cast<int>(pb.variants.size());
         pb.variants.push_back(v);
+        pb.vmac.push_back(mac);
         vindex[key] = id;
         return id;
     };

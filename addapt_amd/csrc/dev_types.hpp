@@ -127,6 +127,9 @@ struct KArgs {
     int Nraw;                   // raw device length
     int Nmax;                   // max folded length over variants
     int cells;                  // (Nmax-4)(Nmax-3)/2
+    const int *groups2;         // [n_groups2][2]: variants folded in lockstep (apo, holo of one
+    int n_groups2;              //   (context, macrostate); a lone variant is paired with itself)
+    int opt;                    // launch-time LDS options (kernels.hip choose_opt)
 };
 
 // Monte Carlo state (device, read/write).

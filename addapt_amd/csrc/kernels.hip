@@ -111,19 +111,27 @@ constexpr int DT_HP = 896;     // [u] hairpin length factor
 constexpr int CHUNK = 16;      // closing-pair cells per chunk of one wave (4 prefetch lanes each)
 constexpr int GSLOTS = NG_MAX / WAVE;   // 6
 constexpr int SSLOTS = NS_MAX / WAVE;   // 2
-constexpr int QSLOTS = (NMAX + 1 + WAVE - 1) / WAVE;  // 4
+constexpr int LDS_LIMIT = 160 * 1024;
 
-// LDS carve-out for one workgroup.  lds_layout() is the single source of the
-// layout: the kernel carves with it and the host sizes the launch with it.
+// LDS carve-out for one workgroup folding P variants in lockstep (P = 2: the
+// apo and holo folds of one (context, macrostate), which share every cell,
+// pair type and loop factor and differ only by the ligand-motif bonus).
+// lds_layout() is the single source of the layout: the kernel carves with it
+// and the host sizes the launch with it.
+template <int P>
 struct Lds {
-    float *qbm, *qm, *qm1;
-    uint8_t *cc;       // inner-pair code per cell (diagonal-major)
-    uint8_t *pcnt;     // [d] pairable cells of diagonal d
+    float *qbm[P], *qm[P], *qm1[P];
+    float *mla[P];     // [2][np] per variant: sum_k qm[i][k-1] qm1[k][j] of the last two qm diagonals
+    float *q5[P];
+    uint8_t *cc;       // inner-pair code per cell (diagonal-major), shared
+    uint8_t *pcnt;     // [d] pairable cells of diagonal d, shared
     uint8_t *wsc;      // [wave][64] i of the cells of a wave's chunk
-    float *mla;        // [2][np] sum_k qm[i][k-1] qm1[k][j] of the last two qm diagonals
+    uint32_t *rec;     // optional (null when it does not fit): per pairable cell, by diagonal and rank:
+                       //   i | oc << 8 | up[i+1] << 16 | dn[j-1] << 24,  oc = type*25 + S[i+1]*5 + S[j-1]
+    uint16_t *rbase;   // with rec: first record of diagonal d
+    uint32_t *rt;      // optional: rt[d * 16 + w] = kb_lo | kb_hi << 8 | km_lo << 16 | km_hi << 24
     float *ct;         // CT_SIZE factor table (DevScaled::ctab)
     float *dt;         // per-cell tables (DT_*)
-    float *q5;
     uint16_t *gd;      // G list: n1 | n2 << 8        (NG_MAX)
     float *gf;         // G list factors               (NG_MAX)
     uint32_t *sd;      // S list: n1 | n2 << 8 | kind << 16 (NS_MAX)
@@ -136,8 +144,9 @@ struct Lds {
 
 // DRY = true: sizes only (host); false: carve `base` (device; no null test, so
 // the pointers stay in the LDS address space)
-template <bool DRY>
-__host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, int nvar, Lds *L) {
+template <bool DRY, int P>
+__host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, int nvar, Lds<P> *L,
+                                             bool with_pl = false, bool with_rt = false) {
     size_t o = 0;
     auto take = [&](size_t bytes) -> char * {
         char *p = DRY ? nullptr : base + o;
@@ -146,17 +155,19 @@ __host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, in
     };
     const size_t C = size_t(cells);
     const int NP = Nmax + 2;
-    Lds l;
-    l.qbm = reinterpret_cast<float *>(take(C * 4));
-    l.qm = reinterpret_cast<float *>(take(C * 4));
-    l.qm1 = reinterpret_cast<float *>(take(C * 4));
+    Lds<P> l;
+    for (int p = 0; p < P; p++) {
+        l.qbm[p] = reinterpret_cast<float *>(take(C * 4));
+        l.qm[p] = reinterpret_cast<float *>(take(C * 4));
+        l.qm1[p] = reinterpret_cast<float *>(take(C * 4));
+        l.mla[p] = reinterpret_cast<float *>(take(2 * NP * 4));
+        l.q5[p] = reinterpret_cast<float *>(take(NP * 4));
+    }
     l.cc = reinterpret_cast<uint8_t *>(take(C));
     l.pcnt = reinterpret_cast<uint8_t *>(take(NP));
     l.wsc = reinterpret_cast<uint8_t *>(take(16 * WAVE));
-    l.mla = reinterpret_cast<float *>(take(2 * NP * 4));
     l.ct = reinterpret_cast<float *>(take(CT_SIZE * 4));
     l.dt = reinterpret_cast<float *>(take(size_t(DT_HP + Nmax + 1) * 4));
-    l.q5 = reinterpret_cast<float *>(take(NP * 4));
     l.gd = reinterpret_cast<uint16_t *>(take(NG_MAX * 2));
     l.gf = reinterpret_cast<float *>(take(NG_MAX * 4));
     l.sd = reinterpret_cast<uint32_t *>(take(NS_MAX * 4));
@@ -171,12 +182,18 @@ __host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, in
     l.flg = reinterpret_cast<uint8_t *>(take(NP));
     l.mat = reinterpret_cast<uint8_t *>(take(NP));
     l.raw = reinterpret_cast<uint8_t *>(take(NP));
+    // pairable cells (i, j), j - i >= 4: S[i] and S[j] sit on opposite sides of the
+    // bipartite pairing graph {A,G} x {C,U}, so there are at most N^2/4 of them
+    l.rec = with_pl ? reinterpret_cast<uint32_t *>(take((size_t(Nmax) * Nmax / 4 + Nmax) * 4)) : nullptr;
+    l.rbase = with_pl ? reinterpret_cast<uint16_t *>(take(size_t(NP) * 2)) : nullptr;
+    l.rt = with_rt ? reinterpret_cast<uint32_t *>(take(size_t(NP) * 16 * 4)) : nullptr;
     l.np = NP;
     if (!DRY) *L = l;
     return o;
 }
 
-__device__ void load_ctab(const KArgs &ka, const Lds &L) {
+template <int P>
+__device__ void load_ctab(const KArgs &ka, const Lds<P> &L) {
     const int NT = blockDim.x;
     for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = ka.X->ctab[k];
     const DevTables &T = *ka.T;
@@ -205,7 +222,8 @@ __device__ void load_ctab(const KArgs &ka, const Lds &L) {
 // ---------------------------------------------------------------- hard constraints
 // flg bits: 1 = 'x' (no pair), 2 = '<' (pairs upstream), 4 = '>' (downstream);
 // ptn = enforced partner (0 none); enc = innermost enclosing enforced pair id.
-__device__ __forceinline__ bool allowed(const Lds &L, int i, int j) {
+template <int P>
+__device__ __forceinline__ bool allowed(const Lds<P> &L, int i, int j) {
     const int fi = L.flg[i], fj = L.flg[j];
     if ((fi | fj) & 1) return false;
     if ((fi & 2) || (fj & 4)) return false;
@@ -226,6 +244,26 @@ __device__ __forceinline__ int cdiv_pos(int x, int y) {
     return uni(q);
 }
 __device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// Sums of two per-lane values over the wave: permlane32 swap folds the halves
+// (lanes 0-31 then carry a, 32-63 carry b), one row/half DPP chain finishes.
+__device__ __forceinline__ void wave_sum2(float a, float b, float &sa, float &sb) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> lane 31 = sum(a), lane 63 = sum(b)
+    sa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
+    sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+template <int P>
+__device__ __forceinline__ void wave_sums(const float (&v)[P], float (&s)[P]) {
+    if constexpr (P == 2) wave_sum2(v[0], v[1], s[0], s[1]);
+    else s[0] = wave_sum(v[0]);
+}
 
 // ---------------------------------------------------------------- closing-pair terms
 // Per-lane descriptors of one span's interior-loop terms (lane t of slot s =
@@ -250,27 +288,37 @@ struct CellU {
     float mmo, tau, mo, m23;
 };
 
-// Sum of the interior-loop terms of (i, j) (before the outer mismatch of the
-// generic loops, which is applied here): SS / SG slots, MK = constrained cell.
-template <int SS, int SG, bool MK>
-__device__ __forceinline__ float qb_terms(const Lds &L, const TermLanes &D, const CellU &u, float gtab) {
-    if (SS == 0) return 0.f;
+// Interior-loop sums of (i, j) for the P variants (the outer mismatch of the
+// generic loops applied here): SS / SG slots, MK = constrained cell.  Every
+// loop factor is computed once and applied to the P tables.
+template <int SS, int SG, bool MK, int P>
+__device__ __forceinline__ void qb_terms(const Lds<P> &L, const TermLanes &D, const CellU &u, float gtab,
+                                         float (&out)[P]) {
+    if (SS == 0) {
+#pragma unroll
+        for (int p = 0; p < P; p++) out[p] = 0.f;
+        return;
+    }
     const float *ct = L.ct;
     const int lane = threadIdx.x & (WAVE - 1);
-    float q[SG > 0 ? SG : 1];
+    float q[P][SG > 0 ? SG : 1];
 #pragma unroll
-    for (int s = 0; s < SG; s++) q[s] = L.qbm[D.offG[s] + u.i];
+    for (int s = 0; s < SG; s++)
+#pragma unroll
+        for (int p = 0; p < P; p++) q[p][s] = L.qbm[p][D.offG[s] + u.i];
     const int ix0 = D.offS[0] + u.i;
-    const float qs0 = L.qbm[ix0];
+    float qs0[P], qs1[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) qs0[p] = L.qbm[p][ix0];
     const int c0 = L.cc[ix0];
-    float qs1 = 0.f;
     int c1 = 0;
     if (SS > 1) {
         const int ix1 = D.offS[1] + u.i;
-        qs1 = L.qbm[ix1];
+#pragma unroll
+        for (int p = 0; p < P; p++) qs1[p] = L.qbm[p][ix1];
         c1 = L.cc[ix1];
     }
-    float g0 = 0.f, g1 = 0.f;
+    float fg[SG > 0 ? SG : 1];
 #pragma unroll
     for (int s = 0; s < SG; s++) {
         float f = D.fG[s];
@@ -278,8 +326,7 @@ __device__ __forceinline__ float qb_terms(const Lds &L, const TermLanes &D, cons
             const int pk = L.gd[s * WAVE + lane];
             f = ((pk & 255) <= u.A && (pk >> 8) <= u.B) ? f : 0.f;
         }
-        if (s & 1) g1 = fmaf(q[s], f, g1);
-        else g0 = fmaf(q[s], f, g0);
+        fg[s] = f;
     }
     // slot 0: stack / bulge 1 / 1x1..2x2 tables / 2x3 / bulges / 1xn
     const int t2 = (c0 * 41) >> 10;
@@ -291,70 +338,98 @@ __device__ __forceinline__ float qb_terms(const Lds &L, const TermLanes &D, cons
         const int pk = int(L.sd[lane]);
         f0 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f0 : 0.f;
     }
-    float sa = qs0 * f0;
+    float f1 = 0.f;
     if (SS > 1) {
         // slot 1: bulges and 1xn only
-        float f1 = ct[D.b1[1] + c1] * (D.fS[1] * fmaf(D.em1, u.mo - u.tau, u.tau));
+        f1 = ct[D.b1[1] + c1] * (D.fS[1] * fmaf(D.em1, u.mo - u.tau, u.tau));
         if (MK) {
             const int pk = int(L.sd[WAVE + lane]);
             f1 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f1 : 0.f;
         }
-        sa = fmaf(qs1, f1, sa);
     }
-    return fmaf(g0 + g1, u.mmo, sa);
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+        float g0 = 0.f, g1 = 0.f;
+#pragma unroll
+        for (int s = 0; s < SG; s++) {
+            if (s & 1) g1 = fmaf(q[p][s], fg[s], g1);
+            else g0 = fmaf(q[p][s], fg[s], g0);
+        }
+        float sa = qs0[p] * f0;
+        if (SS > 1) sa = fmaf(qs1[p], f1, sa);
+        out[p] = fmaf(g0 + g1, u.mmo, sa);
+    }
 }
 
-template <bool MK>
-__device__ __forceinline__ float qb_terms_dispatch(int sS, int sG, const Lds &L, const TermLanes &D,
-                                                   const CellU &u, float gtab) {
+template <bool MK, int P>
+__device__ __forceinline__ void qb_terms_dispatch(int sS, int sG, const Lds<P> &L, const TermLanes &D,
+                                                  const CellU &u, float gtab, float (&out)[P]) {
     if (sS == 2) {
         switch (sG) {
-            case 6: return qb_terms<2, 6, MK>(L, D, u, gtab);
-            case 5: return qb_terms<2, 5, MK>(L, D, u, gtab);
-            case 4: return qb_terms<2, 4, MK>(L, D, u, gtab);
-            case 3: return qb_terms<2, 3, MK>(L, D, u, gtab);
-            default: return qb_terms<2, 2, MK>(L, D, u, gtab);
+            case 6: qb_terms<2, 6, MK, P>(L, D, u, gtab, out); return;
+            case 5: qb_terms<2, 5, MK, P>(L, D, u, gtab, out); return;
+            case 4: qb_terms<2, 4, MK, P>(L, D, u, gtab, out); return;
+            case 3: qb_terms<2, 3, MK, P>(L, D, u, gtab, out); return;
+            default: qb_terms<2, 2, MK, P>(L, D, u, gtab, out); return;
         }
     }
     if (sS == 1) {
         switch (sG) {
-            case 0: return qb_terms<1, 0, MK>(L, D, u, gtab);
-            case 1: return qb_terms<1, 1, MK>(L, D, u, gtab);
-            default: return qb_terms<1, 2, MK>(L, D, u, gtab);
+            case 0: qb_terms<1, 0, MK, P>(L, D, u, gtab, out); return;
+            case 1: qb_terms<1, 1, MK, P>(L, D, u, gtab, out); return;
+            default: qb_terms<1, 2, MK, P>(L, D, u, gtab, out); return;
         }
     }
-    return 0.f;
+    qb_terms<0, 0, MK, P>(L, D, u, gtab, out);
 }
 
-// qm(i, i+sq) split sums over SQ slots of split points t (lanes):
-//   A = sum_{t>=5} qm[i][i+t-1] qm1[i+t][jb],  P = sum_t pw(t) qm1[i+t][jb]
-template <int SQ>
-__device__ __forceinline__ void qm_terms(const float *q1, const float *qr, int tmax, int upi,
-                                         const float *pwr, int lane, float &A, float &P) {
-    float v1[SQ], vr[SQ];
-#pragma unroll
-    for (int q = 0; q < SQ; q++) {
-        const int t = q * WAVE + lane;
-        v1[q] = q1[t <= tmax ? t : tmax];
-        vr[q] = qr[(t <= tmax && t >= 5) ? t : 5];
-    }
-    float a0 = 0.f, p0 = 0.f;
-#pragma unroll
-    for (int q = 0; q < SQ; q++) {
-        const int t = q * WAVE + lane;
-        const bool ok = t <= tmax;
-        const float b = ok ? v1[q] : 0.f;
-        a0 = fmaf((ok && t >= 5) ? vr[q] : 0.f, b, a0);
-        p0 = fmaf((ok && t <= upi) ? pwr[q] : 0.f, b, p0);
-    }
-    A = a0;
-    P = p0;
+// ---------------------------------------------------------------- work split
+// Per-diagonal item counts and estimated costs (x4 units) of iteration d.
+struct RangeCost {
+    int cp, cq, umax, nS, nG, sS, sG, nit, sQ5, cqg, ca, cb, c5, Ct;
+};
+
+template <int P>
+__host__ __device__ inline RangeCost range_cost(int d, int N, int cp) {
+    RangeCost r;
+    const int sq = d - 1;                                   // qm span
+    r.cp = cp;
+    r.cq = (sq >= 4 && sq <= N - 3) ? N - sq : 0;
+    r.umax = d - 6 < 30 ? d - 6 : 30;
+    // |S|, |G| of the terms with u <= umax (dev_types.hpp lists, closed form)
+    r.nS = r.umax < 0 ? 0 : r.umax <= 5 ? ((r.umax + 1) * (r.umax + 2)) / 2 : 21 + 4 * (r.umax - 5);
+    r.nG = r.umax < 6 ? 0 : ((r.umax - 3) * (r.umax - 2)) / 2 - 3;
+    r.sS = (r.nS + WAVE - 1) / WAVE;
+    r.sG = (r.nG + WAVE - 1) / WAVE;
+    r.nit = r.cq ? (sq - 3 + 15) / 16 : 0;                  // qm: 16 lanes per cell
+    r.sQ5 = (d - 4 + WAVE - 1) / WAVE;
+    r.cqg = (r.cq + 3) / 4;                                 // qm items = groups of 4 cells
+    r.ca = (4 * r.sG + 12 * r.sS) * (P + 1) / 2 + 16;
+    r.cb = 6 * r.nit * P + 12;
+    r.c5 = 16 * r.sQ5 + 16;
+    r.Ct = r.c5 + r.cp * r.ca + r.cqg * r.cb;
+    return r;
+}
+
+// Wave w's items: [qb cells][qm groups][q5] cut into NW equal-cost ranges
+// (q5 is last: it belongs to the last wave).  out = kb_lo, kb_hi, km_lo, km_hi.
+template <int NW>
+__device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
+    const int lo = w * rc.Ct, hi = lo + rc.Ct;              // x NW
+    auto cdiv = [](int x, int y) { return x <= 0 ? 0 : (x + y - 1) / y; };
+    out[0] = clampi(cdiv(lo, rc.ca * NW), 0, rc.cp);
+    out[1] = clampi(cdiv(hi, rc.ca * NW), 0, rc.cp);
+    const int b2 = rc.cp * rc.ca;
+    out[2] = 4 * clampi(cdiv(lo - b2 * NW, rc.cb * NW), 0, rc.cqg);
+    out[3] = min(rc.cq, 4 * clampi(cdiv(hi - b2 * NW, rc.cb * NW), 0, rc.cqg));
 }
 
 // ---------------------------------------------------------------- inside PF
-// Per-variant setup pass (all cells at once, no DP dependency):
+// P variants of one (context, macrostate) folded in lockstep (same cells,
+// same pairable set, same factors; the holo variant adds the motif bonus).
+// Per-group setup pass (all cells at once, no DP dependency):
 //   cc    inner-pair code of every cell,
-//   qbm   hairpin (+ ligand motif) factor of every pairable cell, 0 otherwise,
+//   qbm   hairpin (+ ligand motif) factor of every pairable cell,
 //   qm1   multiloop-stem factor of every pairable cell, 0 otherwise,
 //   pcnt  the number of pairable cells of every diagonal.
 // A non-pairable cell keeps qbm = -0.0f for the whole fold (it is never
@@ -368,16 +443,16 @@ __device__ __forceinline__ void qm_terms(const float *q1, const float *qr, int t
 // A closing-pair cell is summed by ONE wave: lanes = terms of its interior-loop
 // lists (S and G, dev_types.hpp), reduced with DPP; its multiloop term is the
 // split sum mla(i+1, j-1) that the qm item of the previous iteration kept.  A qm
-// item is one wave as well (lanes = split points).  Items are cut into NW
-// contiguous ranges of equal estimated cost, one per wave.
-template <int NT>
-__device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds &L,
-                           const DevScaled *__restrict__ XS0) {
+// item is 4 cells x 16 lanes (split points).  Items are cut into NW contiguous
+// ranges of equal estimated cost, one per wave.
+template <int NT, int P>
+__device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, const Lds<P> &L,
+                         const DevScaled *__restrict__ XS, float (&z)[P]) {
     constexpr int NW = NT / WAVE;
-    // opaque copies: keep the compiler from hoisting dozens of derived 64-bit
-    // addresses out of the variant loop (they spill SGPRs)
-    const DevScaled *__restrict__ XS = XS0;
-    const DevVariant V = ka.variants[v];
+    const DevVariant V = ka.variants[vs[0]];
+    bool motif[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) motif[p] = ka.variants[vs[p]].motif != 0;
     const int N = uni(V.N);
     const float *ct = L.ct;
     const int tid = threadIdx.x;
@@ -385,7 +460,7 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     const int wid = uni(tid / WAVE);
     const int NP = L.np;
 
-    // ---- per-variant setup: sequence, constraint arrays, motif sites
+    // ---- per-group setup: sequence, constraint arrays, motif sites
     const uint8_t *cons = ka.cons + V.cons_off;
     const int np = N + 2;
     const uint8_t *bef = nullptr, *aft = nullptr;
@@ -399,10 +474,10 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     for (int k = tid; k < np; k += NT) {
         uint8_t s = 0;
         if (k >= 1 && k <= N) {
-            const int p = k - 1;
-            if (p < blen) s = bef[p];
-            else if (p < blen + ka.Nraw) s = raw[p - blen];
-            else s = aft[p - blen - ka.Nraw];
+            const int pp = k - 1;
+            if (pp < blen) s = bef[pp];
+            else if (pp < blen + ka.Nraw) s = raw[pp - blen];
+            else s = aft[pp - blen - ka.Nraw];
         }
         L.S[k] = s;
         const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k];
@@ -414,15 +489,20 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
         L.mat[k] = 0;
         if (k >= 1 && k <= N && (f || pt)) constrained = true;
     }
-    for (int k = tid; k < 2 * NP; k += NT) L.mla[k] = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; p++)
+        for (int k = tid; k < 2 * NP; k += NT) L.mla[p][k] = 0.f;
     constrained = __syncthreads_or(constrained);
     if (tid == 0) {
         // ViennaRNA's S1 wrap-around (only reaches values that are never used)
         L.S[0] = L.S[N];
         L.S[N + 1] = L.S[1];
     }
+    bool any_motif = false;
+#pragma unroll
+    for (int p = 0; p < P; p++) any_motif |= motif[p];
     const int mL = XS->motif_len;
-    if (V.motif && mL > 0) {
+    if (any_motif && mL > 0) {
         for (int o = tid + 1; o + mL - 1 <= N; o += NT) {
             bool ok = true;
             for (int k = 0; k < mL && ok; k++) {
@@ -441,12 +521,14 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     const float mlbase_sig = XS->mlbase_sig;
     const float mlclosing = XS->mlclosing;
     const float eTAU = XS->ctab[CT_FSM + 6];
-    const int mlen = V.motif ? mL : 0;
     const float mextra = XS->motif_extra;
     const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
     if (tid == 0) {
-        L.q5[0] = 1.0f;
-        for (int j = 1; j <= 3 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] * sig1 : 0.f;
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            L.q5[p][0] = 1.0f;
+            for (int j = 1; j <= 3 && j <= N; j++) L.q5[p][j] = (L.up[j] >= 1) ? L.q5[p][j - 1] * sig1 : 0.f;
+        }
     }
     // cells of every diagonal: wave w takes diagonals 4 + w, 4 + w + NW, ...
     for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
@@ -464,6 +546,7 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
                 const int type = ptype(si, sj);
                 pr = type != 0 && allowed(L, i, j);
                 float h = 0.f, m1 = 0.f;
+                bool mx = false;
                 if (pr) {
                     if (L.up[i + 1] >= u) {
                         h = -1.f;
@@ -476,19 +559,68 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
                             h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type]
                                                             : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
                     }
-                    if (dd == mlen - 1 && L.mat[i]) h += mextra;
+                    mx = dd == mL - 1 && mL > 0 && L.mat[i];
                     m1 = L.dt[DT_MLS + type * 25 + sim * 5 + sjp];
                 }
-                L.qbm[od + r] = pr ? h : -0.0f;
+#pragma unroll
+                for (int p = 0; p < P; p++) {
+                    L.qbm[p][od + r] = pr ? ((mx && motif[p]) ? h + mextra : h) : -0.0f;
+                    L.qm1[p][colb(j) + i - 1] = m1;
+                }
                 L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
-                L.qm1[colb(j) + i - 1] = m1;
             }
             base += __popcll(__ballot(pr));
         }
         if (lane == 0) L.pcnt[dd] = static_cast<uint8_t>(base);
     }
-
     __syncthreads();
+    if (L.rec) {
+        // record offsets: exclusive prefix sum of pcnt over the diagonals (wave 0)
+        if (wid == 0) {
+            int carry = 0;
+            for (int d0 = 0; d0 < N; d0 += WAVE) {
+                const int dd = d0 + lane;
+                const int own = (dd >= 4 && dd <= N - 1) ? int(L.pcnt[dd]) : 0;
+                int v = own;
+#pragma unroll
+                for (int o = 1; o < WAVE; o <<= 1) {
+                    const int t = __shfl_up(v, o, WAVE);
+                    if (lane >= o) v += t;
+                }
+                if (dd <= N) L.rbase[dd] = static_cast<uint16_t>(carry + v - own);
+                carry += __shfl(v, WAVE - 1, WAVE);
+            }
+        }
+        __syncthreads();
+        // the records, in rank order per diagonal
+        for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
+            const int c = N - dd, od = off(dd, N), rb = L.rbase[dd];
+            int base = 0;
+            for (int r0 = 0; r0 < c; r0 += WAVE) {
+                const int r = r0 + lane;
+                const bool pr = r < c && __float_as_uint(L.qbm[0][od + r]) != 0x80000000u;
+                const unsigned long long bm = __ballot(pr);
+                if (pr) {
+                    const int i = r + 1, j = i + dd;
+                    const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+                    L.rec[rb + base + __popcll(bm & ((1ull << lane) - 1ull))] =
+                        uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) | (uint32_t(L.dn[j - 1]) << 24);
+                }
+                base += __popcll(bm);
+            }
+        }
+    }
+    // item ranges of every (diagonal, wave): rt, or computed in prep() when rt does not fit
+    if (L.rt) {
+        for (int t = tid; t < (N - 3) * NW; t += NT) {
+            const int d = 4 + t / NW, w = t % NW;
+            RangeCost rc = range_cost<P>(d, N, d <= N - 1 ? int(L.pcnt[d]) : 0);
+            int r[4];
+            wave_range<NW>(rc, w, r);
+            L.rt[d * 16 + w] = uint32_t(r[0]) | (uint32_t(r[1]) << 8) | (uint32_t(r[2]) << 16) | (uint32_t(r[3]) << 24);
+        }
+    }
+    if (L.rt || L.rec) __syncthreads();
 
     // ---------------- loop-carried state.  prep(d) runs at the end of
     // iteration d-1 (before its barrier) and fills everything iteration d needs
@@ -499,7 +631,10 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     int kb_lo = 0, kb_hi = 0, km_lo = 0, km_hi = 0;
     // closing-pair chunk (lanes = cells of the chunk)
     int ci = 1, cty = 0, cA = 0, cB = 0, cidx = 0, cm1 = 0;
-    float cmmo = 0.f, ctau = 1.f, cmo = 0.f, cm23 = 0.f, cmmc = 0.f, cpre = 0.f, cpm1 = 0.f, cmlc = 0.f, pfx = 0.f;
+    float cmmo = 0.f, ctau = 1.f, cmo = 0.f, cm23 = 0.f, cmmc = 0.f, cpm1 = 0.f, cmlc = 0.f, pfx = 0.f;
+    float cpre[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) cpre[p] = 0.f;
     uint8_t *ws = L.wsc + wid * WAVE;
     // term descriptors: offsets advance by k - d per diagonal once every term is
     // valid (d > 36); before that they are recomputed
@@ -533,11 +668,16 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     // lanes c < nc: cell kc + c (rank among the pairable cells of diagonal d)
     auto load_chunk = [&](int d, int kc, int nc) {
         const int od = off(d, N);
-        {   // ballot scan of the non-pairable mark -> ws[rank - kc] = i
+        uint32_t wc, wp;   // record words of cell `lane` and of cell `lane / 4` of the chunk
+        if (L.rec) {
+            const int rb = L.rbase[d] + kc;
+            wc = L.rec[rb + (lane < nc ? lane : nc - 1)];
+            wp = L.rec[rb + ((lane >> 2) < nc ? (lane >> 2) : nc - 1)];
+        } else {   // ballot scan of the non-pairable mark -> ws[rank - kc] = i
             int base = 0;
             for (int r0 = 0; r0 < N - d && base < kc + nc; r0 += WAVE) {
                 const int r = r0 + lane;
-                const bool pr = r < N - d && __float_as_uint(L.qbm[od + r]) != 0x80000000u;
+                const bool pr = r < N - d && __float_as_uint(L.qbm[0][od + r]) != 0x80000000u;
                 const unsigned long long m = __ballot(pr);
                 const int rank = base + __popcll(m & ((1ull << lane) - 1ull));
                 if (pr && rank >= kc && rank < kc + nc) ws[rank - kc] = static_cast<uint8_t>(r + 1);
@@ -546,36 +686,44 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            auto word = [&](int i) {
+                const int j = i + d;
+                const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+                return uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) | (uint32_t(L.dn[j - 1]) << 24);
+            };
+            wc = word(ws[lane < nc ? lane : nc - 1]);
+            wp = word(ws[(lane >> 2) < nc ? (lane >> 2) : nc - 1]);
         }
         {
-            const int c = lane < nc ? lane : nc - 1;
-            const int i = ws[c], j = i + d;
-            const int si1 = L.S[i + 1], sj1 = L.S[j - 1];
+            const int i = wc & 255, j = i + d;
+            const int oc = (wc >> 8) & 255;
+            const int ty = (oc * 41) >> 10, si1 = (oc / 5) % 5, sj1 = oc % 5;
             ci = i;
-            cty = ptype(L.S[i], L.S[j]);
-            cA = L.up[i + 1];
-            cB = L.dn[j - 1];
-            const int oc = cty * 25 + si1 * 5 + sj1;
+            cty = ty;
+            cA = (wc >> 16) & 255;
+            cB = wc >> 24;
             cmmo = L.dt[DT_MMI + oc];
-            ctau = cty > 2 ? eTAU : 1.f;
+            ctau = ty > 2 ? eTAU : 1.f;
             cmo = ct[CT_ONEN + oc] * cmmo;
             cm23 = ct[CT_M23O + oc];
             cidx = od + i - 1;
             cmmc = L.dt[DT_MMI + L.cc[cidx]];
-            cpre = L.qbm[cidx];
+#pragma unroll
+            for (int p = 0; p < P; p++) cpre[p] = L.qbm[p][cidx];
             cm1 = colb(j) + i - 1;
-            cpm1 = L.qm1[cm1];
-            cmlc = mlclosing * L.dt[DT_MLS + rtype(cty) * 25 + sj1 * 5 + si1];
+            cpm1 = L.qm1[0][cm1];
+            cmlc = mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + sj1 * 5 + si1];
         }
         {   // lane 4c + g: the 1x1 / 1x2 / 2x1 / 2x2 table factor g of cell c (HBM/L2)
             const int c = lane >> 2, g = lane & 3;
             const int n1 = (g >= 2) ? 2 : 1, n2 = (g & 1) ? 2 : 1;
             pfx = 0.f;
             if (c < nc && n1 + n2 <= umax) {
-                const int i = ws[c], j = i + d;
-                const int typ = ptype(L.S[i], L.S[j]);
+                const int i = wp & 255, j = i + d;
+                const int oc = (wp >> 8) & 255;
+                const int typ = (oc * 41) >> 10, a1 = (oc / 5) % 5, b1 = oc % 5;
                 const int t2 = (L.cc[off(d - 2 - n1 - n2, N) + i + n1] * 41) >> 10;
-                const int a1 = L.S[i + 1], b1 = L.S[j - 1], sp1 = L.S[i + n1], sq1 = L.S[j - n2];
+                const int sp1 = (n1 == 1) ? a1 : L.S[i + 2], sq1 = (n2 == 1) ? b1 : L.S[j - 2];
                 const float *src;
                 if (g == 0) src = &T.int11[typ][t2][a1][b1];
                 else if (g == 1) src = &T.int21[typ][t2][a1][sq1][b1];
@@ -587,27 +735,29 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     };
 
     auto prep = [&](int d) {
-        // item ranges of this wave (estimated cost, x4)
-        const int sq = d - 1;                                   // qm span
-        cp = uni((d <= N - 1) ? L.pcnt[d] : 0);
-        cq = (sq >= 4 && sq <= N - 3) ? N - sq : 0;
-        umax = d - 6 < 30 ? d - 6 : 30;
-        // |S|, |G| of the terms with u <= umax (dev_types.hpp lists, closed form)
-        const int nS = umax < 0 ? 0 : umax <= 5 ? ((umax + 1) * (umax + 2)) / 2 : 21 + 4 * (umax - 5);
-        const int nG = umax < 6 ? 0 : ((umax - 3) * (umax - 2)) / 2 - 3;
-        sS = (nS + WAVE - 1) / WAVE;
-        sG = (nG + WAVE - 1) / WAVE;
-        nit = cq ? (sq - 3 + 15) / 16 : 0;                      // qm: 16 lanes per cell
-        sQ5 = (d - 4 + WAVE - 1) / WAVE;
-        const int cqg = (cq + 3) / 4;                           // qm items = groups of 4 cells
-        const int ca = 4 * sG + 12 * sS + 16, cb = 6 * nit + 12, c5 = 16 * sQ5 + 16;
-        const int Ct = c5 + cp * ca + cqg * cb;
-        const int lo = wid * Ct, hi = lo + Ct;                  // x NW
-        kb_lo = clampi(cdiv_pos(lo - c5 * NW, ca * NW), 0, cp);
-        kb_hi = clampi(cdiv_pos(hi - c5 * NW, ca * NW), 0, cp);
-        const int b2 = c5 + cp * ca;
-        km_lo = 4 * clampi(cdiv_pos(lo - b2 * NW, cb * NW), 0, cqg);
-        km_hi = min(cq, 4 * clampi(cdiv_pos(hi - b2 * NW, cb * NW), 0, cqg));
+        const RangeCost rc = range_cost<P>(d, N, uni((d <= N - 1) ? L.pcnt[d] : 0));
+        cp = rc.cp;
+        cq = rc.cq;
+        umax = rc.umax;
+        sS = rc.sS;
+        sG = rc.sG;
+        nit = rc.nit;
+        sQ5 = rc.sQ5;
+        const int nS = rc.nS, nG = rc.nG;
+        if (L.rt) {
+            const uint32_t e = uni(int(L.rt[d * 16 + wid]));
+            kb_lo = e & 255;
+            kb_hi = (e >> 8) & 255;
+            km_lo = (e >> 16) & 255;
+            km_hi = e >> 24;
+        } else {
+            int r[4];
+            wave_range<NW>(rc, wid, r);
+            kb_lo = uni(r[0]);
+            kb_hi = uni(r[1]);
+            km_lo = uni(r[2]);
+            km_hi = uni(r[3]);
+        }
         // term descriptors of span d
         if (d <= 36) {
 #pragma unroll
@@ -645,43 +795,29 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
         const int sq = d - 1;
         // ---------------- values iteration d-1 wrote: qm1(i, j-1) and mla(i+1, j-1)
         // of the first chunk; qm1 of the non-pairable cells of d (stored at the end)
-        float cprev = 0.f, cml = 0.f;
-        if (kb_lo < kb_hi) {
+        float cprev[P], cml[P];
+        auto late = [&]() {
             const int j = ci + d;
-            cprev = (d >= 5 && L.up[j] >= 1) ? L.qm1[colb(j - 1) + ci - 1] : 0.f;
-            cml = L.mla[((d - 2) & 1) * NP + ci + 1] * cmlc;
-        }
+            const bool upj = d >= 5 && L.up[j] >= 1;
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                cprev[p] = upj ? L.qm1[p][colb(j - 1) + ci - 1] : 0.f;
+                cml[p] = L.mla[p][((d - 2) & 1) * NP + ci + 1] * cmlc;
+            }
+        };
+        if (kb_lo < kb_hi) late();
         const int r1 = tid, i1 = r1 + 1, j1 = i1 + d;
         const bool has1 = r1 < N - d;
-        float m1pre = 1.f, m1prev = 0.f;
+        bool m1np = false;    // non-pairable: the -0 mark (a finalized cell is never -0)
+        float m1prev[P];
         int m1up = 0;
         if (has1) {
-            m1pre = L.qm1[colb(j1) + i1 - 1];
-            m1prev = L.qm1[colb(j1 - 1) + i1 - 1];
+            m1np = __float_as_uint(L.qbm[0][off(d, N) + i1 - 1]) == 0x80000000u;
+#pragma unroll
+            for (int p = 0; p < P; p++) m1prev[p] = L.qm1[p][colb(j1 - 1) + i1 - 1];
             m1up = L.up[j1];
         }
         STAMP(0);
-
-        // ---------------- q5[d] (wave 0)
-        if (wid == 0) {
-            const int j = d;
-            const int sjp = (j < N) ? L.S[j + 1] : 5;
-            const int sj = L.S[j];
-            float acc = 0.f;
-            for (int q = 0; q < sQ5; q++) {
-                const int k0 = q * WAVE + lane + 1;
-                const bool ok = k0 <= j - 4;
-                const int k = ok ? k0 : 1;
-                const int ix = off(j - k, N) + k - 1;
-                const int ty = ptype(L.S[k], sj);
-                const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + sjp];
-                const float x = L.q5[k - 1] * L.qbm[ix];
-                acc = fmaf(x, ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f, acc);
-            }
-            const float sum = wave_sum(acc);
-            if (lane == 0) L.q5[j] = ((L.up[j] >= 1) ? L.q5[j - 1] * sig1 : 0.f) + sum;
-        }
-        STAMP(6);
 
         // ---------------- qm(i, i+sq) and mla(i, sq), groups of 4 cells,
         // 16 lanes (split points t = it*16 + l16) per cell:
@@ -694,37 +830,37 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
                 const bool cell = m < km_hi;
                 const int i = m + 1, jb = i + sq;
                 const int upi = constrained ? L.up[cell ? i : 1] : 255;
-                const float *q1 = L.qm1 + colb(jb) + i - 1;
-                const float *qr = L.qm + rowb(i, N) - 5;
-                float A0 = 0.f, P0 = 0.f, A1 = 0.f, P1 = 0.f;
+                const int o1 = colb(jb) + i - 1, orr = rowb(i, N) - 5;
+                float A[P], Pp[P];
+#pragma unroll
+                for (int p = 0; p < P; p++) { A[p] = 0.f; Pp[p] = 0.f; }
                 int it = 0;
-                for (; it + 2 <= nit; it += 2) {
-                    const int t0 = it * 16 + l16, t1 = t0 + 16;
-                    const bool ok0 = cell && t0 <= tmax, ok1 = cell && t1 <= tmax;
-                    const float v0 = q1[ok0 ? t0 : 0], v1 = q1[ok1 ? t1 : 0];
-                    const float r0 = qr[(ok0 && t0 >= 5) ? t0 : 5], r1v = qr[(ok1 && t1 >= 5) ? t1 : 5];
-                    const float w0 = L.pw[t0 <= N ? t0 : N], w1 = L.pw[t1 <= N ? t1 : N];
-                    const float b0 = ok0 ? v0 : 0.f, b1 = ok1 ? v1 : 0.f;
-                    A0 = fmaf((ok0 && t0 >= 5) ? r0 : 0.f, b0, A0);
-                    A1 = fmaf((ok1 && t1 >= 5) ? r1v : 0.f, b1, A1);
-                    P0 = fmaf((t0 <= upi) ? w0 : 0.f, b0, P0);
-                    P1 = fmaf((t1 <= upi) ? w1 : 0.f, b1, P1);
-                }
-                if (it < nit) {
+#ifdef ADX_ABL_QM
+                it = nit;
+#endif
+                for (; it < nit; it++) {
                     const int t0 = it * 16 + l16;
                     const bool ok0 = cell && t0 <= tmax;
-                    const float v0 = q1[ok0 ? t0 : 0];
-                    const float r0 = qr[(ok0 && t0 >= 5) ? t0 : 5];
+                    const bool okr = ok0 && t0 >= 5;
                     const float w0 = L.pw[t0 <= N ? t0 : N];
-                    const float b0 = ok0 ? v0 : 0.f;
-                    A0 = fmaf((ok0 && t0 >= 5) ? r0 : 0.f, b0, A0);
-                    P0 = fmaf((t0 <= upi) ? w0 : 0.f, b0, P0);
+                    const float pw0 = (t0 <= upi) ? w0 : 0.f;
+#pragma unroll
+                    for (int p = 0; p < P; p++) {
+                        const float v0 = L.qm1[p][o1 + (ok0 ? t0 : 0)];
+                        const float r0 = L.qm[p][orr + (okr ? t0 : 5)];
+                        const float b0 = ok0 ? v0 : 0.f;
+                        A[p] = fmaf(okr ? r0 : 0.f, b0, A[p]);
+                        Pp[p] = fmaf(pw0, b0, Pp[p]);
+                    }
                 }
-                const float sA = row_sum(A0 + A1);
-                const float sP = row_sum(P0 + P1);
-                if (l16 == 15 && cell) {
-                    L.qm[rowb(i, N) + sq - 4] = sA + sP;
-                    L.mla[(sq & 1) * NP + i] = sA;
+#pragma unroll
+                for (int p = 0; p < P; p++) {
+                    const float sA = row_sum(A[p]);
+                    const float sP = row_sum(Pp[p]);
+                    if (l16 == 15 && cell) {
+                        L.qm[p][rowb(i, N) + sq - 4] = sA + sP;
+                        L.mla[p][(sq & 1) * NP + i] = sA;
+                    }
                 }
             }
         }
@@ -735,11 +871,11 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
             const int nc = (kb_hi - kc) < CHUNK ? kb_hi - kc : CHUNK;
             if (kc != kb_lo) {
                 load_chunk(d, kc, nc);
-                const int j = ci + d;
-                cprev = (d >= 5 && L.up[j] >= 1) ? L.qm1[colb(j - 1) + ci - 1] : 0.f;
-                cml = L.mla[((d - 2) & 1) * NP + ci + 1] * cmlc;
+                late();
             }
-            float sums = 0.f;
+            float sums[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) sums[p] = 0.f;
             for (int c = 0; c < nc; c++) {
                 CellU u;
                 u.i = __builtin_amdgcn_readlane(ci, c);
@@ -753,19 +889,66 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
                 const bool masked = constrained && (u.A < umax || u.B < umax);
                 // gather of the prefetched 1x1..2x2 table factors for this cell
                 const float gtab = __shfl(pfx, c * 4 + D.gsel, WAVE);
-                const float part = masked ? qb_terms_dispatch<true>(sS, sG, L, D, u, gtab)
-                                          : qb_terms_dispatch<false>(sS, sG, L, D, u, gtab);
-                const float tot = wave_sum(part);
-                sums = (lane == c) ? tot : sums;
+                float part[P], tot[P];
+#ifndef ADX_ABL_QBT
+                if (masked) qb_terms_dispatch<true, P>(sS, sG, L, D, u, gtab, part);
+                else qb_terms_dispatch<false, P>(sS, sG, L, D, u, gtab, part);
+#else
+#pragma unroll
+                for (int p = 0; p < P; p++) part[p] = gtab * 0.f;
+#endif
+                wave_sums<P>(part, tot);
+#pragma unroll
+                for (int p = 0; p < P; p++) sums[p] = (lane == c) ? tot[p] : sums[p];
             }
             if (lane < nc) {
-                const float qb = sums + cpre + cml;
-                L.qbm[cidx] = qb * cmmc + 0.0f;   // never -0 (the non-pairable mark)
-                L.qm1[cm1] = fmaf(qb, cpm1, cprev * mlbase_sig);
+#pragma unroll
+                for (int p = 0; p < P; p++) {
+                    const float qb = sums[p] + cpre[p] + cml[p];
+                    L.qbm[p][cidx] = qb * cmmc + 0.0f;   // never -0 (the non-pairable mark)
+                    L.qm1[p][cm1] = fmaf(qb, cpm1, cprev[p] * mlbase_sig);
+                }
             }
         }
-        if (has1 && m1pre == 0.f) L.qm1[colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? m1prev * mlbase_sig : 0.f;
         STAMP(4);
+
+        // ---------------- q5[d] (the last wave: q5 is last in the cost order)
+#ifndef ADX_ABL_Q5
+        if (wid == NW - 1) {
+#else
+        if (false) {
+#endif
+            const int j = d;
+            const int sjp = (j < N) ? L.S[j + 1] : 5;
+            const int sj = L.S[j];
+            float acc[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) acc[p] = 0.f;
+            for (int q = 0; q < sQ5; q++) {
+                const int k0 = q * WAVE + lane + 1;
+                const bool ok = k0 <= j - 4;
+                const int k = ok ? k0 : 1;
+                const int ix = off(j - k, N) + k - 1;
+                const int ty = ptype(L.S[k], sj);
+                const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + sjp];
+                const float f = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
+#pragma unroll
+                for (int p = 0; p < P; p++) acc[p] = fmaf(L.q5[p][k - 1] * L.qbm[p][ix], f, acc[p]);
+            }
+            float sum[P];
+            wave_sums<P>(acc, sum);
+            if (lane == 0) {
+#pragma unroll
+                for (int p = 0; p < P; p++)
+                    L.q5[p][j] = ((L.up[j] >= 1) ? L.q5[p][j - 1] * sig1 : 0.f) + sum[p];
+            }
+        }
+        STAMP(6);
+        if (has1 && m1np) {
+#pragma unroll
+            for (int p = 0; p < P; p++)
+                L.qm1[p][colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? m1prev[p] * mlbase_sig : 0.f;
+        }
         if (d < N) prep(d + 1);
         STAMP(7);
         __syncthreads();
@@ -775,12 +958,14 @@ __device__ float pf_inside(const KArgs &ka, int v, const uint8_t *raw, const Lds
     if (lane == 0 && wid < 16)
         for (int k = 0; k < 12; k++) atomicAdd(&g_stamps[wid][k], st_acc[k]);
 #endif
-    return L.q5[N];   // scaled Z; the energy is taken after the variant loop
+#pragma unroll
+    for (int p = 0; p < P; p++) z[p] = L.q5[p][N];   // scaled Z; energies after the group loop
 }
 
 // ---------------------------------------------------------------- scoring
 // lane 0 of the block: score from the per-variant energies in L.G
-__device__ double combine_score(const KArgs &ka, const Lds &L, double *terms_out) {
+template <int P>
+__device__ double combine_score(const KArgs &ka, const Lds<P> &L, double *terms_out) {
     const DevScaled &X = *ka.X;
     double score = 0.0;
     for (int c = 0; c < ka.n_ctx_eff; c++) {
@@ -799,14 +984,26 @@ __device__ double combine_score(const KArgs &ka, const Lds &L, double *terms_out
     return score;
 }
 
-template <int NT>
+template <int NT, int P>
 __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
-                                 const uint8_t *raw, const Lds &L,
+                                 const uint8_t *raw, const Lds<P> &L,
                                  float *dG_out, double *terms_out) {
-    for (int v = 0; v < ka.n_variants; v++) {
-        const float z = pf_inside<NT>(ka, v, raw, L, XS);
-        if (threadIdx.x == 0) L.G[v] = static_cast<double>(z);
-        __syncthreads();   // the next variant rewrites the tables
+    const int ng = P == 2 ? ka.n_groups2 : ka.n_variants;
+    for (int g = 0; g < ng; g++) {
+        int vs[P];
+        if constexpr (P == 2) {
+            vs[0] = ka.groups2[2 * g];
+            vs[1] = ka.groups2[2 * g + 1];
+        } else {
+            vs[0] = g;
+        }
+        float z[P];
+        pf_group<NT, P>(ka, vs, raw, L, XS, z);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int p = 0; p < P; p++) L.G[vs[p]] = static_cast<double>(z[p]);
+        }
+        __syncthreads();   // the next group rewrites the tables
     }
     double s = 0.0;
     if (threadIdx.x == 0) {
@@ -822,13 +1019,13 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
     return s;
 }
 
-template <int NT>
-__global__ void __launch_bounds__(NT, 4)
+template <int NT, int P>
+__global__ void __launch_bounds__(NT, (NT == 768) ? 3 : 4)
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    Lds L;
-    lds_layout<false>(smem, ka.cells, ka.Nmax, ka.n_variants, &L);
+    Lds<P> L;
+    lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, (ka.opt & 1) != 0, (ka.opt & 2) != 0);
     const int w = blockIdx.x;
     if (w >= W) return;
     if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
@@ -836,8 +1033,8 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
-    const double s = score_sequence<NT>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
-                                             terms ? terms + size_t(w) * nt : nullptr);
+    const double s = score_sequence<NT, P>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
+                                          terms ? terms + size_t(w) * nt : nullptr);
     if (threadIdx.x == 0) scores[w] = s;
 }
 
@@ -1051,16 +1248,53 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 }  // namespace
 
 // ---------------------------------------------------------------- host launchers
-size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
-    return lds_layout<true>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr);
+// P = 2 (apo/holo lockstep, 16 waves) when its LDS fits one CU, else P = 1
+// (8 waves, two workgroups per CU when they fit).
+#ifndef ADX_NT2
+#define ADX_NT2 768     // 12 waves x 168 VGPRs (16 x 128 spills)
+#endif
+template <int P>
+static size_t lds_size(const KArgs &ka, bool pl, bool rt) {
+    return lds_layout<true, P>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, pl, rt);
 }
 
-constexpr int NT_DEFAULT = 512;
+static int choose_p(const KArgs &ka) {
+#ifdef ADX_FORCE_P1
+    return 1;
+#endif
+    return lds_size<2>(ka, false, false) <= size_t(LDS_LIMIT) ? 2 : 1;
+}
 
-hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
-                          float *dG, const int *mask, hipStream_t stream) {
-    const size_t lds = lds_bytes(ka, true, NT_DEFAULT);
-    auto k = score_kernel<NT_DEFAULT>;
+// optional LDS arrays (rank list, range table) when they still fit
+template <int P>
+static void choose_opt(const KArgs &ka, bool &pl, bool &rt) {
+    // P = 1 keeps two workgroups per CU when they fit (1 KiB margin for allocation granularity)
+    const size_t lim = (P == 1 && 2 * lds_size<1>(ka, false, false) <= size_t(LDS_LIMIT) - 2048)
+                           ? LDS_LIMIT / 2 - 1024 : LDS_LIMIT;
+    rt = lds_size<P>(ka, false, true) <= lim;
+    pl = lds_size<P>(ka, true, rt) <= lim;
+#ifdef ADX_NO_OPT
+    pl = rt = false;
+#endif
+}
+
+size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
+    bool pl, rt;
+    if (choose_p(ka) == 2) {
+        choose_opt<2>(ka, pl, rt);
+        return lds_size<2>(ka, pl, rt);
+    }
+    choose_opt<1>(ka, pl, rt);
+    return lds_size<1>(ka, pl, rt);
+}
+
+template <int NT, int P>
+static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
+                                 float *dG, const int *mask, hipStream_t stream) {
+    bool pl, rt;
+    choose_opt<P>(ka, pl, rt);
+    const size_t lds = lds_size<P>(ka, pl, rt);
+    auto k = score_kernel<NT, P>;
     static size_t configured = 0;
     if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
@@ -1068,8 +1302,16 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         if (e != hipSuccess) return e;
         configured = lds;
     }
-    hipLaunchKernelGGL(k, dim3(W), dim3(NT_DEFAULT), lds, stream, ka, ka.X, seqs, W, scores, terms, dG, mask);
+    KArgs kb = ka;
+    kb.opt = (pl ? 1 : 0) | (rt ? 2 : 0);
+    hipLaunchKernelGGL(k, dim3(W), dim3(NT), lds, stream, kb, kb.X, seqs, W, scores, terms, dG, mask);
     return hipGetLastError();
+}
+
+hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
+                          float *dG, const int *mask, hipStream_t stream) {
+    if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2>(ka, seqs, W, scores, terms, dG, mask, stream);
+    return launch_score_t<512, 1>(ka, seqs, W, scores, terms, dG, mask, stream);
 }
 
 hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, double *scores,

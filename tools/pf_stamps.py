@@ -23,5 +23,5 @@ V = eng.info.n_variants
 cols = [(10, "top"), (0, "late"), (6, "q5"), (5, "qm"), (4, "qb"), (7, "prep"), (9, "barrier")]
 print("cycles per PF per wave (avg over %d variants)" % V)
 print("wave " + " ".join("%9s" % n for _, n in cols))
-for w in range(8):
+for w in range(16):
     print("%4d " % w + " ".join("%9d" % (buf[w * 16 + k] // V) for k, _ in cols))
