@@ -61,12 +61,13 @@ def build_host(force=False):
         return None
     os.makedirs(OBJ, exist_ok=True)
     inc = os.path.join(ROOT, "include")
-    headers = glob.glob(os.path.join(inc, "addapt", "*.hh")) + [os.path.join(inc, "addapt_gpu.h")]
+    headers = (glob.glob(os.path.join(inc, "addapt", "*.hh")) + [os.path.join(inc, "addapt_gpu.h")] +
+               glob.glob(os.path.join(HOSTSRC, "*.hh")))
     lib = os.path.join(OUT, "libaddapt_host.so")
     lib_srcs = [s for s in srcs if not os.path.basename(s).startswith("app_")]
     if force or _newer(lib_srcs + headers, lib):
-        _run(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-I", inc, "-o", lib] + lib_srcs +
-             ["-L", OUT, "-laddapt_gpu", "-Wl,-rpath,$ORIGIN"])
+        _run(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-I", inc, "-I", HOSTSRC,
+              "-o", lib] + lib_srcs + ["-L", OUT, "-laddapt_gpu", "-ldl", "-Wl,-rpath,$ORIGIN"])
     for app in [s for s in srcs if os.path.basename(s).startswith("app_")]:
         exe = os.path.join(OUT, os.path.basename(app)[4:-3])
         if force or _newer([app, lib] + headers, exe):

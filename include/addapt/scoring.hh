@@ -1,0 +1,125 @@
+// addapt-amd C++ host API: folding and scoring (reference include/scoring.hh).
+//
+//   RnaFold            abstract fold (scoring.hh:42-55)
+//   GpuRnaFold         ViennaRnaFold's role (scoring.cc:17-103), folds on the
+//                      MI355X through the per-fold C ABI (adx_fold_*)
+//   ScoreTerm / MacrostateProbTerm / ScoreFunction   (scoring.hh:94-192)
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "addapt/model.hh"
+
+namespace addapt {
+
+class ScoreFunction;
+using ScoreFunctionPtr = std::shared_ptr<ScoreFunction>;
+class ScoreTerm;
+using ScoreTermPtr = std::shared_ptr<ScoreTerm>;
+using ScoreTermList = std::vector<ScoreTermPtr>;
+
+struct EvaluatedScoreTerm {
+    string name;
+    double weight, term;
+};
+using EvaluatedScoreFunction = std::vector<EvaluatedScoreTerm>;
+
+enum class ConditionEnum { APO, HOLO };
+enum class FavorableEnum { NO, YES };
+
+class RnaFold {
+public:
+    virtual ~RnaFold() = default;
+    virtual double base_pair_prob(int i, int j) const = 0;
+    virtual double macrostate_prob(string constraint) const = 0;
+};
+
+/// Energy parameters shared by every GPU fold (ViennaRNA 2.0 file layout).
+void set_parameter_file(const string &path);
+/// kT at 37 C in kcal/mol (scoring.cc:69-70).
+double kT();
+
+class GpuRnaFold : public RnaFold {
+public:
+    explicit GpuRnaFold(DeviceConstPtr device, AptamerConstPtr aptamer = nullptr, int gpu = 0);
+    double base_pair_prob(int i, int j) const override;
+    double macrostate_prob(string constraint) const override;
+
+private:
+    string seq_;
+    AptamerConstPtr aptamer_;
+    int gpu_;
+};
+using ViennaRnaFold = GpuRnaFold;   // the reference's name for this role
+
+class ScoreTerm {
+public:
+    explicit ScoreTerm(string name = "", double weight = 1.0) : name_(name), weight_(weight) {}
+    virtual ~ScoreTerm() = default;
+    virtual double evaluate(DeviceConstPtr device, RnaFold const &apo, RnaFold const &holo) const = 0;
+    string name() const { return name_; }
+    void name(string n) { name_ = n; }
+    double weight() const { return weight_; }
+    void weight(double w) { weight_ = w; }
+
+private:
+    string name_;
+    double weight_;
+};
+
+/// ln P(macrostate) (or ln(1-P) if not favorable) in the apo or holo fold
+/// (scoring.cc:233-259); name "apo: x" / "holo: not x".
+class MacrostateProbTerm : public ScoreTerm {
+public:
+    MacrostateProbTerm(string macrostate, ConditionEnum cond, FavorableEnum fav = FavorableEnum::YES);
+    double evaluate(DeviceConstPtr device, RnaFold const &apo, RnaFold const &holo) const override;
+    string macrostate() const { return macrostate_; }
+    ConditionEnum condition() const { return condition_; }
+    FavorableEnum favorable() const { return favorable_; }
+
+private:
+    string macrostate_;
+    ConditionEnum condition_;
+    FavorableEnum favorable_;
+};
+
+/// Factory for the folds a score function evaluates with (GpuRnaFold by
+/// default; tests substitute their own, as the reference tests do with
+/// DummyRnaFold).
+using FoldFactory = std::shared_ptr<RnaFold> (*)(DeviceConstPtr, AptamerConstPtr);
+
+class ScoreFunction {
+public:
+    ScoreFunction();
+    double evaluate(DeviceConstPtr device) const;
+    virtual double evaluate(DeviceConstPtr device, EvaluatedScoreFunction &table) const;
+    void add_term(ScoreTermPtr t) { terms_.push_back(t); }
+    void operator+=(ScoreTermPtr t) { add_term(t); }
+    const ScoreTermList &terms() const { return terms_; }
+    AptamerConstPtr aptamer() const { return aptamer_; }
+    void aptamer(AptamerConstPtr a) { aptamer_ = a; }
+    ContextConstPtr context(string name) const;
+    void add_context(string name, ContextConstPtr c) { contexts_[name] = c; }
+    const std::map<string, ContextConstPtr> &contexts() const { return contexts_; }
+    void fold_factory(FoldFactory f) { factory_ = f; }
+    virtual ~ScoreFunction() = default;
+
+protected:
+    double evaluate_terms(DeviceConstPtr device, EvaluatedScoreFunction &table, string prefix = "") const;
+
+private:
+    ScoreTermList terms_;
+    AptamerConstPtr aptamer_;
+    std::map<string, ContextConstPtr> contexts_;
+    FoldFactory factory_;
+};
+
+}  // namespace addapt
+
+namespace std {
+ostream &operator<<(ostream &, const addapt::ConditionEnum &);
+ostream &operator<<(ostream &, const addapt::FavorableEnum &);
+}  // namespace std

@@ -1,0 +1,112 @@
+"""The C++ host mirror and CLI on the GPU: the addapt command line on the
+reference's rhf(6) device and default objective (BASELINE config 1 plumbing)
+against the oracle's MonteCarlo::apply, through the fused engine and
+through the reference loop (per-fold C ABI)."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from addapt_amd import workloads
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "addapt_amd", "_lib", "addapt")
+OUTC = {"REJECT": 0, "ACCEPT_WORSENED": 1, "ACCEPT_UNCHANGED": 2, "ACCEPT_IMPROVED": 3}
+
+CONFIG = """\
+sequence: {seq}
+macrostates:
+  active: '{act}'
+objective:
+  apo: not active
+  holo: active
+aptamer:
+  sequence: GAUACCAGCCGAAAGGCCCUUGGCAGC
+  fold: (...((.(((....)))....))...)
+  affinity: 0.32
+thermostat: 5 to 0 in 300 steps
+"""
+
+
+def _config(tmp_path):
+    p = tmp_path / "rhf6.yml"
+    p.write_text(CONFIG.format(seq=workloads.RHF6_SEQ, act=workloads.RHF6_ACTIVE))
+    return str(p)
+
+
+def _read_tsv(path):
+    lines = open(path).read().splitlines()
+    assert lines[0].startswith("#\tinitial_seq\t")
+    head = lines[1].rstrip("\t").split("\t")
+    rows = [dict(zip(head, l.rstrip("\t").split("\t"))) for l in lines[2:]]
+    return head, rows
+
+
+def _run(args, timeout=600):
+    r = subprocess.run([EXE] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+@pytest.mark.gpu
+def test_cli_trajectory_matches_oracle(oracle, tmp_path):
+    cfg = _config(tmp_path)
+    out = str(tmp_path / "traj.tsv")
+    steps = 60
+    _run([cfg, "-n", str(steps), "-r", "0", "-o", out])
+    head, rows = _read_tsv(out)
+    assert len(rows) == steps
+    assert "term_value[apo: not active]" in head and "term_value[holo: active]" in head
+    outc = [OUTC[r["outcome"]] for r in rows]
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
+    th = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    ref = oracle.mc_run(sf, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], th, 0, steps, forced=outc,
+                        tie_eps=1e-6, want_seqs=True)
+    assert ref["rc"] == 0
+    assert outc == ref["outcome"]
+    for s, r in enumerate(rows):
+        assert r["current_seq"] == ref["seqs"][s], s
+        # the TSV prints with ostream's default 6 significant digits, as the reference
+        assert float(r["temperature"]) == pytest.approx(ref["temperature"][s], rel=1e-5, abs=1e-9)
+        if outc[s] != 2:
+            assert float(r["proposed_score"]) == pytest.approx(ref["proposed_score"][s], abs=2e-3)
+            assert float(r["random_threshold"]) == pytest.approx(ref["random_threshold"][s], rel=1e-5)
+
+
+@pytest.mark.gpu
+def test_cli_reference_loop_matches_engine(tmp_path):
+    cfg = _config(tmp_path)
+    a, b = str(tmp_path / "engine.tsv"), str(tmp_path / "loop.tsv")
+    _run([cfg, "-n", "12", "-r", "5", "-o", a])
+    _run([cfg, "-n", "12", "-r", "5", "-o", b, "--reference-loop"])
+    _, ra = _read_tsv(a)
+    _, rb = _read_tsv(b)
+    assert [r["outcome"] for r in ra] == [r["outcome"] for r in rb]
+    assert [r["current_seq"] for r in ra] == [r["current_seq"] for r in rb]
+    for x, y in zip(ra, rb):
+        assert float(x["current_score"]) == pytest.approx(float(y["current_score"]), abs=2e-3)
+
+
+@pytest.mark.gpu
+def test_cli_batched_walkers(oracle, tmp_path):
+    cfg = _config(tmp_path)
+    out = str(tmp_path / "walkers.tsv")
+    W, steps = 16, 30
+    _run([cfg, "-n", str(steps), "-r", "100", "--walkers", str(W), "-o", out])
+    lines = open(out).read().splitlines()
+    assert len(lines) == W + 1
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
+    for l in lines[1:]:
+        f = l.split("\t")
+        counts = [int(x) for x in f[3:7]]
+        assert sum(counts) == steps
+        seq = f[7]
+        ref, _ = sf.score(seq, [workloads.RHF6_ACTIVE])
+        assert float(f[2]) == pytest.approx(ref, abs=2e-3)
+        # frozen (lower-case) positions never change
+        assert all(a == b for a, b in zip(seq, workloads.RHF6_SEQ) if b.islower())
