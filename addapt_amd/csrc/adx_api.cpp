@@ -1074,6 +1074,35 @@ extern "C" adx_status adx_walkers_download(adx_ctx *c, char *seqs, double *score
     return ADX_OK;
 }
 
+extern "C" adx_status adx_walkers_export(adx_ctx *c, void *dev_seqs, void *dev_scores) {
+    if (!c) return fail(ADX_EINVAL, "adx_walkers_export: null context");
+    if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
+    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
+    if (dev_seqs) HIP_TRY(hipMemcpyAsync(dev_seqs, c->cur_seq.p, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_scores)
+        HIP_TRY(hipMemcpyAsync(dev_scores, c->cur_score.p, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
+    HIP_TRY(hipStreamSynchronize(c->pb.stream));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_walkers_import(adx_ctx *c, const void *dev_seqs, const void *dev_scores) {
+    if (!c) return fail(ADX_EINVAL, "adx_walkers_import: null context");
+    if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
+    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
+    if (dev_seqs) HIP_TRY(hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_scores)
+        HIP_TRY(hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
+    HIP_TRY(hipStreamSynchronize(c->pb.stream));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_set_temperature(adx_ctx *c, double t) {
+    if (!c) return fail(ADX_EINVAL, "adx_set_temperature: null context");
+    if (c->thermo.kind != ADX_THERMO_FIXED) return fail(ADX_EINVAL, "adx_set_temperature: not a fixed thermostat");
+    c->thermo.t_fixed = t;
+    return ADX_OK;
+}
+
 extern "C" adx_status adx_score_batch(adx_ctx *c, int W, const char *seqs, double *scores,
                                       double *term_values, float *dG) {
     if (!c || W <= 0 || !seqs || !scores) return fail(ADX_EINVAL, "adx_score_batch: bad argument");

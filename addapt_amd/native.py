@@ -70,7 +70,8 @@ EXPORTS = [
     "adx_eval_structure", "adx_fold_create", "adx_fold_add_motif", "adx_fold_add_constraint",
     "adx_fold_pf", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
     "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
-    "adx_walkers_download", "adx_score_batch", "adx_variant_desc",
+    "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
+    "adx_walkers_import", "adx_set_temperature",
 ]
 
 _lib = None
@@ -102,6 +103,9 @@ def lib():
         L.adx_run_steps.argtypes = [C.c_void_p, C.c_int, C.POINTER(Trace)]
         L.adx_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         L.adx_last_score_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+        L.adx_walkers_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.adx_walkers_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.adx_set_temperature.argtypes = [C.c_void_p, C.c_double]
         L.adx_walkers_download.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
                                            C.POINTER(C.c_int64)]
         L.adx_score_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_double),
@@ -294,6 +298,17 @@ class Engine:
         ms = C.c_double()
         _check(lib().adx_last_kernel_ms(self.ptr, C.byref(ms)))
         return ms.value
+
+    def export_walkers(self, dev_seqs_ptr, dev_scores_ptr):
+        """Device-to-device copy of the walkers' sequence codes (W*N uint8) and
+        scores (W float64) into caller-owned device buffers (raw pointers)."""
+        _check(lib().adx_walkers_export(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+
+    def import_walkers(self, dev_seqs_ptr, dev_scores_ptr):
+        _check(lib().adx_walkers_import(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+
+    def set_temperature(self, t):
+        _check(lib().adx_set_temperature(self.ptr, float(t)))
 
     def last_score_kernel_ms(self):
         """(average score-kernel launch ms, launches) of the last run_steps."""

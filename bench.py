@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="approximate budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--replica-interval", type=int, default=0,
+                    help="BASELINE config 5: one temperature rung per rank (0.5*1.5^r), RCCL swap of "
+                         "walker configurations between neighbouring rungs every K steps (N > 1 only)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic")
     return ap.parse_args()
@@ -89,7 +92,14 @@ def main():
     tmpl, active = workloads.synthetic(a.length)
     terms = workloads.default_objective()
     apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
-    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    replica_mode = a.replica_interval > 0 and world > 1
+    if replica_mode:
+        from addapt_amd import replica
+
+        temps = replica.ladder_temperatures(world)
+        th = native.make_thermostat("fixed", t=temps[rank])
+    else:
+        th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank)
     W = a.walkers
     gids = shard.walker_ids(rank, world, W)
@@ -108,7 +118,11 @@ def main():
     _, _, c0 = eng.download()
     barrier()
     t0 = time.perf_counter()
-    eng.run_steps(a.steps)
+    if replica_mode:
+        rx = replica.run(eng, dist, rank, world, a.steps, a.replica_interval, temps, seed=0,
+                         device="cuda")
+    else:
+        eng.run_steps(a.steps)
     barrier()
     t1 = time.perf_counter()
     kernel_ms = eng.last_kernel_ms()            # whole timed run_steps (3 kernels per step)
@@ -126,7 +140,7 @@ def main():
     f_free = sum(roofline.pf_flops(s, None) for s in sample) / len(sample)
     f_act = sum(roofline.pf_flops(s, active) for s in sample) / len(sample)
     flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
-    launch_flops = scored * flop_per_scored / max(1, launches)      # per score launch
+    launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
     achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
     traffic, traffic_src = None, None
     if a.traffic_json and os.path.exists(a.traffic_json):
@@ -150,10 +164,10 @@ def main():
         "all_kernels_ms_per_step": kernel_ms / a.steps,
         "flop_per_scored_step": flop_per_scored,
         "flop_per_launch": launch_flops,
-        "scored_walkers_per_launch": scored / max(1, launches),
+        "scored_walkers_per_launch": scored / max(1, a.steps),
         # compulsory HBM bytes of one launch: each scored walker reads its
         # proposal (N B) and writes its score (8 B)
-        "algorithmic_bytes_per_launch": (scored / max(1, launches)) * (a.length + 8),
+        "algorithmic_bytes_per_launch": (scored / max(1, a.steps)) * (a.length + 8),
     }
     out = {
         "metric": METRIC,
@@ -176,7 +190,9 @@ def main():
             "walkers_per_gpu": W,
             "global_walkers": W * world,
             "length": a.length,
-            "parallelism": "walker-sharded x%d (no data-path collective)" % world,
+            "parallelism": ("replica exchange x%d (RCCL neighbour swap every %d steps)"
+                            % (world, a.replica_interval)) if replica_mode
+            else "walker-sharded x%d (no data-path collective)" % world,
             "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, outcomes)},
         },
         "roofline": roof,

@@ -180,6 +180,18 @@ adx_status adx_last_score_kernel_ms(const adx_ctx *ctx, double *avg_ms, int *lau
 
 adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
 
+/* Replica exchange (BASELINE config 5): copy the walkers' configurations --
+ * sequence codes (W*N bytes, 1..4 = A,C,G,U) and scores (W doubles) -- to or
+ * from caller-owned DEVICE buffers on the context's GPU (e.g. torch tensors
+ * swapped between ranks over RCCL).  RNG streams, counters and thermostat
+ * state stay with the walker slot: a swap moves configurations between
+ * temperatures.  Synchronous; the caller's own writes to the buffers must be
+ * complete (its stream synchronized) before adx_walkers_import. */
+adx_status adx_walkers_export(adx_ctx *ctx, void *dev_seqs, void *dev_scores);
+adx_status adx_walkers_import(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores);
+/* Temperature of an ADX_THERMO_FIXED context (one rung of a replica ladder). */
+adx_status adx_set_temperature(adx_ctx *ctx, double t);
+
 /* Parity entry point: score W sequences (W*N chars) without moving.
  * scores[W]; term_values[W*n_terms*max(1,n_contexts)] (optional);
  * dG[W*n_variants] ensemble energies (kcal/mol, float, optional). */

@@ -1,0 +1,88 @@
+"""Replica-exchange rounds (addapt_amd/replica.py) across 2 and 3 CPU ranks
+(gloo): both ranks of a pair take the same decisions, configurations are
+conserved, and the acceptance rule is the detailed-balance one."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from addapt_amd import replica
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, N, rounds, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(1000 + rank)
+        seqs = torch.randint(1, 5, (W, N), dtype=torch.uint8, generator=g)
+        seqs[:, 0] = rank        # tag: which rung the configuration started on
+        scores = -torch.rand(W, dtype=torch.float64, generator=g) * 5.0 - rank
+        start = (seqs.clone(), scores.clone())
+        temps = replica.ladder_temperatures(world)
+        stats = []
+        for r in range(rounds):
+            stats.append(replica.exchange_round(dist, r, rank, world, temps, seqs, scores, seed=7))
+        q.put((rank, start, (seqs, scores), stats))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_rounds_conserve_configurations(world):
+    W, N, rounds = 64, 12, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, N, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=180)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # every (sequence, score) configuration survives exactly once per slot
+    for w in range(W):
+        before = sorted((bytes(res[r][1][0][w].tolist()), float(res[r][1][1][w])) for r in range(world))
+        after = sorted((bytes(res[r][2][0][w].tolist()), float(res[r][2][1][w])) for r in range(world))
+        assert before == after
+    acc = sum(s[1] for r in range(world) for s in res[r][3])
+    assert acc > 0
+
+
+def test_swap_rule():
+    t_lo, t_hi = 0.5, 0.75
+    # the higher-scoring configuration always moves down to the colder rung
+    assert replica.swap_accept(1, 0, 0, [-5.0], [-1.0], t_lo, t_hi).all()
+    # and the reverse move is accepted with probability exp((S_hi - S_lo)(1/T_lo - 1/T_hi))
+    n = 20000
+    s_lo, s_hi = np.full(n, -1.0), np.full(n, -2.0)
+    frac = replica.swap_accept(3, 1, 0, s_lo, s_hi, t_lo, t_hi).mean()
+    assert abs(frac - math.exp(-1.0 * (1 / t_lo - 1 / t_hi))) < 0.02
+    # same key -> same decisions on both ranks of the pair
+    a = replica.swap_accept(9, 4, 2, s_lo[:50], s_hi[:50], t_lo, t_hi)
+    b = replica.swap_accept(9, 4, 2, s_lo[:50], s_hi[:50], t_lo, t_hi)
+    assert (a == b).all()
+    assert not replica.swap_accept(0, 0, 0, [float("nan")], [0.0], t_lo, t_hi).any()
+
+
+def test_pairing():
+    assert [replica.partner(r, 4, 0) for r in range(4)] == [1, 0, 3, 2]
+    assert [replica.partner(r, 4, 1) for r in range(4)] == [None, 2, 1, None]
+    assert replica.ladder_temperatures(3) == [0.5, 0.75, 1.125]

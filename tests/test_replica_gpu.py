@@ -1,0 +1,93 @@
+"""Replica exchange on the GPU: the engine's export / import of walker
+configurations and a 2-rung ladder (2 processes on cuda:0, gloo for the
+exchange -- RCCL needs one GPU per rank; the 8-GPU node uses RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from addapt_amd import workloads
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_export_import_roundtrip(native):
+    tmpl, active = workloads.synthetic(60)
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt,
+                        thermostat=native.make_thermostat("fixed", t=1.0))
+    seqs = workloads.walker_sequences(tmpl, [active], 8)
+    eng.walkers_init(list(range(8)), seqs)
+    t_seqs = torch.empty((8, eng.N), dtype=torch.uint8, device="cuda")
+    t_sc = torch.empty((8,), dtype=torch.float64, device="cuda")
+    eng.export_walkers(t_seqs.data_ptr(), t_sc.data_ptr())
+    s0, sc0, _ = eng.download()
+    code = {1: "A", 2: "C", 3: "G", 4: "U"}
+    assert "".join(code[int(x)] for x in t_seqs[3].cpu()) == s0[3].upper()
+    assert np.allclose(t_sc.cpu().numpy(), sc0)
+    # swap walkers 0 and 1 through the device buffers
+    perm = torch.tensor([1, 0, 2, 3, 4, 5, 6, 7], device="cuda")
+    p_seqs, p_sc = t_seqs[perm].contiguous(), t_sc[perm].contiguous()
+    torch.cuda.synchronize()   # import reads on the engine's stream
+    eng.import_walkers(p_seqs.data_ptr(), p_sc.data_ptr())
+    s1, sc1, _ = eng.download()
+    assert s1[0] == s0[1] and s1[1] == s0[0] and sc1[0] == sc0[1]
+    eng.run_steps(3)
+    _, _, c = eng.download()
+    assert (c.sum(axis=1) == 3).all()
+
+
+def _rung(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from addapt_amd import native, replica
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tmpl, active = workloads.synthetic(60)
+        apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+        eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt,
+                            thermostat=native.make_thermostat("fixed", t=1.0))
+        W = 16
+        ids = list(range(rank * W, (rank + 1) * W))
+        eng.walkers_init(ids, workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + ids[0]))
+        stats = replica.run(eng, dist, rank, world, steps=20, interval=5,
+                            temps=replica.ladder_temperatures(world), seed=3)
+        seqs, scores, counters = eng.download()
+        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+        sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
+        err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in range(W))
+        q.put((rank, stats, float(err), int(counters.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rung_ladder():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rung, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, stats, err, n in res:
+        assert stats["rounds"] == 4
+        assert err <= 2e-3          # imported scores still describe the imported sequences
+        assert n == 16 * 20
+    assert res[0][1]["attempted"] > 0
