@@ -108,6 +108,8 @@ double orc_eval_structure(const orc_params *P, const char *seq, const char *stru
 /* Minimum free energy (integer dcal/mol, lxc truncated as in ViennaRNA's MFE
  * recursions); writes the MFE structure if structure != NULL (N+1 bytes). */
 int orc_mfe(const orc_params *P, const char *seq, const char *constraint, char *structure);
+/* MFE (kcal/mol) with the ligand motif, min-plus image of the PF model (fold.c) */
+double orc_mfe_energy(const orc_params *P, const char *seq, const char *constraint, const orc_motif *motif);
 
 /* ---- RNG -------------------------------------------------------------- */
 typedef struct orc_mt {
@@ -156,6 +158,7 @@ typedef struct orc_scorefxn {
     const orc_motif *aptamer; /* NULL = no aptamer: holo folds like apo */
     int n_contexts;           /* 0 = no contexts; else in std::map (name) order */
     const orc_context *contexts;
+    int mode;                 /* 0 = partition functions (vrna_pf), 1 = MFE (A17) */
 } orc_scorefxn;
 
 /* ScoreFunction::evaluate; term_values (n_terms * max(1,n_contexts)) and

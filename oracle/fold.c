@@ -198,6 +198,7 @@ typedef struct {
     const char *mseq;
     double m_extra; /* Boltzmann extra weight for a formed motif (unscaled) */
     double m_Eint;
+    double m_beff;  /* bonus applied to the formed motif (kcal; mode REPLACE: minus Eint) */
 } model_t;
 
 static int can_pair(const model_t *m, int i, int j) {
@@ -257,6 +258,7 @@ static int model_init(model_t *m, const orc_params *P, const char *seq, const ch
         m->m_Eint = eint;
         double beff = motif->mode == 1 ? motif->energy_kcal - eint : motif->energy_kcal;
         m->m_extra = boltz(eint * 100.0) * (boltz(beff * 100.0) - 1.0);
+        m->m_beff = beff;
     }
     return 1;
 }
@@ -771,4 +773,98 @@ int orc_mfe(const orc_params *P, const char *seq, const char *constraint, char *
     free(c); free(fm); free(fm1); free(f5);
     model_free(&m);
     return result;
+}
+
+/* ------------------------------------------------- MFE with the motif */
+/* Minimum free energy (kcal/mol) of the same model the partition function
+ * sums over, for the engine's MFE fold mode: the min-plus
+ * form of the inside recursion of orc_mfe above, in double so that the
+ * ligand motif can enter like it does in the partition function -- a formed
+ * motif's closing cell may take the motif structure's energy plus the bonus,
+ * c(i,j) = min(c(i,j), Eint + bonus) (the min-plus image of the extra term
+ * exp(-Eint)(exp(-bonus) - 1) the PF adds at the same cell). */
+double orc_mfe_energy(const orc_params *P, const char *seq, const char *constraint,
+                      const orc_motif *motif) {
+    model_t m;
+    if (!model_init(&m, P, seq, constraint, motif)) {
+        model_free(&m);
+        return NAN;
+    }
+    const int N = m.N;
+    const int *S = m.S;
+    const int *up = m.hc.up;
+    const double INF = 1e30;
+    size_t sz = (size_t)(N + 2) * (N + 2);
+    double *c = (double *)malloc(sz * sizeof(double));
+    double *fm = (double *)malloc(sz * sizeof(double));
+    double *fm1 = (double *)malloc(sz * sizeof(double));
+    double *f5 = (double *)malloc((N + 2) * sizeof(double));
+    for (size_t k = 0; k < sz; k++) { c[k] = INF; fm[k] = INF; fm1[k] = INF; }
+    for (int d = ORC_TURN + 1; d <= N - 1; d++) {
+        for (int i = 1; i + d <= N; i++) {
+            int j = i + d;
+            double best = INF;
+            if (can_pair(&m, i, j)) {
+                int type = PAIR[S[i]][S[j]];
+                int u = j - i - 1;
+                if (up[i + 1] >= u) best = E_hairpin_int(P, i, j, S, m.useq);
+                for (int p = i + 1; p <= i + ORC_MAXLOOP + 1 && p < j - ORC_TURN - 1; p++) {
+                    int n1 = p - i - 1;
+                    if (n1 > 0 && up[i + 1] < n1) break;
+                    int minq = j - 1 - (ORC_MAXLOOP - n1);
+                    if (minq < p + ORC_TURN + 1) minq = p + ORC_TURN + 1;
+                    for (int q = j - 1; q >= minq; q--) {
+                        int n2 = j - q - 1;
+                        if (n2 > 0 && up[q + 1] < n2) break;
+                        if (!can_pair(&m, p, q) || c[IDX(p, q)] >= INF) continue;
+                        int type2 = PAIR[S[q]][S[p]];
+                        double e = (int)E_int(P, n1, n2, type, type2, S[i + 1], S[j - 1], S[p - 1], S[q + 1]);
+                        if (c[IDX(p, q)] + e < best) best = c[IDX(p, q)] + e;
+                    }
+                }
+                int tt = RTYPE[type];
+                double sm = INF;
+                for (int k = i + 2; k <= j - 1; k++)
+                    if (fm[IDX(i + 1, k - 1)] < INF && fm1[IDX(k, j - 1)] < INF &&
+                        fm[IDX(i + 1, k - 1)] + fm1[IDX(k, j - 1)] < sm)
+                        sm = fm[IDX(i + 1, k - 1)] + fm1[IDX(k, j - 1)];
+                if (sm < INF && sm + P->MLclosing + E_ml_stem(P, tt, S[j - 1], S[i + 1]) < best)
+                    best = sm + P->MLclosing + E_ml_stem(P, tt, S[j - 1], S[i + 1]);
+                if (m.mL && motif_at(&m, i, j)) {
+                    double e = 100.0 * (m.m_Eint + m.m_beff);
+                    if (e < best) best = e;
+                }
+                c[IDX(i, j)] = best;
+            }
+            double v = INF;
+            if (c[IDX(i, j)] < INF) v = c[IDX(i, j)] + E_ml_stem(P, PAIR[S[i]][S[j]], S[i - 1], S[j + 1]);
+            if (up[j] >= 1 && fm1[IDX(i, j - 1)] < INF && fm1[IDX(i, j - 1)] + P->MLbase < v)
+                v = fm1[IDX(i, j - 1)] + P->MLbase;
+            fm1[IDX(i, j)] = v;
+            double w = INF;
+            for (int k = i; k <= j; k++) {
+                if (fm1[IDX(k, j)] >= INF) continue;
+                double pre = INF;
+                if (k == i || up[i] >= k - i) pre = (double)(k - i) * P->MLbase;
+                if (k > i && fm[IDX(i, k - 1)] < pre) pre = fm[IDX(i, k - 1)];
+                if (pre < INF && pre + fm1[IDX(k, j)] < w) w = pre + fm1[IDX(k, j)];
+            }
+            fm[IDX(i, j)] = w;
+        }
+    }
+    f5[0] = 0.0;
+    for (int j = 1; j <= N; j++) {
+        double v = (up[j] >= 1 && f5[j - 1] < INF) ? f5[j - 1] : INF;
+        for (int k = 1; k + ORC_TURN + 1 <= j; k++) {
+            if (c[IDX(k, j)] >= INF || f5[k - 1] >= INF) continue;
+            int type = PAIR[S[k]][S[j]];
+            double e = f5[k - 1] + c[IDX(k, j)] + E_ext_stem(P, type, k > 1 ? S[k - 1] : -1, j < N ? S[j + 1] : -1);
+            if (e < v) v = e;
+        }
+        f5[j] = v;
+    }
+    double r = f5[N] >= INF ? INFINITY : f5[N] / 100.0;
+    free(c); free(fm); free(fm1); free(f5);
+    model_free(&m);
+    return r;
 }

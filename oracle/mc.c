@@ -144,7 +144,15 @@ static double evaluate_terms(const orc_scorefxn *sf, const char *seq, const char
     for (int t = 0; t < sf->n_terms; t++) {
         const orc_term *T = &sf->terms[t];
         const orc_motif *motif = (T->condition == 1) ? sf->aptamer : NULL;
-        double p = macrostate_prob(sf->P, seq, ms[T->macrostate], motif);
+        double p;
+        if (sf->mode == 1) {
+            /* MFE image of macrostate_prob: float-rounded like vrna_mfe's return */
+            double gt = (float)orc_mfe_energy(sf->P, seq, NULL, motif);
+            double ga = (float)orc_mfe_energy(sf->P, seq, ms[T->macrostate], motif);
+            p = exp((gt - ga) / (orc_kT_cal() / 1000.0));
+        } else {
+            p = macrostate_prob(sf->P, seq, ms[T->macrostate], motif);
+        }
         if (!T->favorable) p = 1.0 - p;
         double v = log(p);
         if (tv) tv[t] = v;

@@ -41,7 +41,7 @@ class Context(C.Structure):
 class ScoreFxn(C.Structure):
     _fields_ = [("P", C.c_void_p), ("n_terms", C.c_int), ("terms", C.POINTER(Term)),
                 ("aptamer", C.POINTER(Motif)), ("n_contexts", C.c_int),
-                ("contexts", C.POINTER(Context))]
+                ("contexts", C.POINTER(Context)), ("mode", C.c_int)]
 
 
 class Thermostat(C.Structure):
@@ -77,6 +77,8 @@ def lib():
         L.orc_params_load.restype = C.c_void_p
         L.orc_params_load.argtypes = [C.c_char_p]
         L.orc_last_error.restype = C.c_char_p
+        L.orc_mfe_energy.restype = C.c_double
+        L.orc_mfe_energy.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(Motif)]
         L.orc_pf_energy.restype = C.c_double
         L.orc_pf_energy.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.POINTER(Motif)]
         L.orc_pf_energy_counted.restype = C.c_double
@@ -188,6 +190,13 @@ def eval_structure(seq, structure, params=None):
     return lib().orc_eval_structure(P.ptr, _b(seq), _b(structure))
 
 
+def mfe_energy(seq, constraint=None, motif=None, params=None):
+    """MFE (kcal/mol) incl. the ligand motif (fold.c orc_mfe_energy)."""
+    P = params or default_params()
+    return lib().orc_mfe_energy(P.ptr, _b(seq), _b(constraint) if constraint else None,
+                                C.byref(motif) if motif is not None else None)
+
+
 def mfe(seq, constraint=None, params=None):
     P = params or default_params()
     buf = C.create_string_buffer(len(seq) + 1)
@@ -232,7 +241,7 @@ def can_be_freely_mutated(seq, macrostates, pos):
 class ScoreFunction:
     """terms: list of (condition 'apo'/'holo', macrostate index, favorable bool, weight)."""
 
-    def __init__(self, terms, aptamer=None, contexts=None, params=None):
+    def __init__(self, terms, aptamer=None, contexts=None, params=None, mode="pf"):
         self.P = params or default_params()
         self._terms = (Term * max(1, len(terms)))()
         for k, (cond, mi, fav, w) in enumerate(terms):
@@ -244,7 +253,8 @@ class ScoreFunction:
         for k, (b, a) in enumerate(ctx):
             self._ctx[k] = Context(_b(b), _b(a))
         self.s = ScoreFxn(self.P.ptr, len(terms), self._terms,
-                          C.pointer(aptamer) if aptamer is not None else None, len(ctx), self._ctx)
+                          C.pointer(aptamer) if aptamer is not None else None, len(ctx), self._ctx,
+                          {"pf": 0, "mfe": 1}[mode])
 
     def score(self, seq, macrostates):
         nt = self.s.n_terms * max(1, self.s.n_contexts)
