@@ -89,30 +89,46 @@ double boltz_d(double e_dcal) {
 }
 float boltz(double e_dcal) { return static_cast<float>(boltz_d(e_dcal)); }
 
-void build_tables(const EnergyParams &P, DevTables &T) {
-    std::memset(&T, 0, sizeof T);
+// Loop factor of energy e (dcal/mol) spanning k scaled nucleotides: the
+// Boltzmann factor exp(-e/kT) sigma^k (partition function) or the energy
+// itself (MFE; INF_E and above -> MFE_BIG).  dev_types.hpp "Fold modes".
+struct Fac {
+    bool mfe;
+    double sigma;
+    float operator()(double e, int k = 0) const {
+        if (mfe) return e >= INF_E ? MFE_BIG : static_cast<float>(e);
+        return static_cast<float>(boltz_d(e) * std::pow(sigma, k));
+    }
+    float zero() const { return mfe ? MFE_BIG : 0.f; }
+    float one() const { return mfe ? 0.f : 1.f; }
+};
+
+void build_tables(const EnergyParams &P, DevTables &T, bool mfe) {
+    const Fac F{mfe, 1.0};
+    float *flat = reinterpret_cast<float *>(&T);
+    for (size_t k = 0; k < sizeof(DevTables) / sizeof(float); k++) flat[k] = F.zero();
     for (int a = 1; a <= 7; a++) {
-        for (int b = 1; b <= 7; b++) T.stack[a][b] = boltz(P.stack[a][b]);
+        for (int b = 1; b <= 7; b++) T.stack[a][b] = F(P.stack[a][b]);
         for (int x = 0; x < 5; x++)
             for (int y = 0; y < 5; y++) {
-                T.mmH[a][x][y] = boltz(P.mmH[a][x][y]);
-                T.mmI[a][x][y] = boltz(P.mmI[a][x][y]);
-                T.mm1n[a][x][y] = boltz(P.mm1nI[a][x][y]);
-                T.mm23[a][x][y] = boltz(P.mm23I[a][x][y]);
-                T.mlstem[a][x][y] = boltz(ml_stem_energy(P, a, x, y));
+                T.mmH[a][x][y] = F(P.mmH[a][x][y]);
+                T.mmI[a][x][y] = F(P.mmI[a][x][y]);
+                T.mm1n[a][x][y] = F(P.mm1nI[a][x][y]);
+                T.mm23[a][x][y] = F(P.mm23I[a][x][y]);
+                T.mlstem[a][x][y] = F(ml_stem_energy(P, a, x, y));
             }
         for (int x = 0; x < 6; x++)
             for (int y = 0; y < 6; y++)
-                T.ext[a][x][y] = boltz(ext_stem_energy(P, a, x == 5 ? -1 : x, y == 5 ? -1 : y));
-        T.termAU[a] = boltz(a > 2 ? P.TermAU : 0);
+                T.ext[a][x][y] = F(ext_stem_energy(P, a, x == 5 ? -1 : x, y == 5 ? -1 : y));
+        T.termAU[a] = F(a > 2 ? P.TermAU : 0);
         for (int b = 1; b <= 7; b++)
             for (int x = 0; x < 5; x++)
                 for (int y = 0; y < 5; y++) {
-                    T.int11[a][b][x][y] = boltz(P.int11[a][b][x][y]);
+                    T.int11[a][b][x][y] = F(P.int11[a][b][x][y]);
                     for (int z = 0; z < 5; z++) {
-                        T.int21[a][b][x][y][z] = boltz(P.int21[a][b][x][y][z]);
+                        T.int21[a][b][x][y][z] = F(P.int21[a][b][x][y][z]);
                         for (int w = 0; w < 5; w++)
-                            T.int22[a][b][x][y][z][w] = boltz(P.int22[a][b][x][y][z][w]);
+                            T.int22[a][b][x][y][z][w] = F(P.int22[a][b][x][y][z][w]);
                     }
                 }
     }
@@ -170,13 +186,22 @@ adx_status prepare_motif(const EnergyParams &P, const Motif &m, double &eint, st
 }
 
 void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double eint,
-                  const std::vector<int> &mpt, DevScaled &X) {
+                  const std::vector<int> &mpt, DevScaled &X, bool mfe) {
     std::memset(&X, 0, sizeof X);
+    const Fac F{mfe, sigma};
     auto sp = [&](int k) { return std::pow(sigma, k); };
     float *ct = X.ctab;
     // code = rtype*25 + S[q+1]*5 + S[p-1] of an inner pair; mismatchI[type2][sq1][sp1]
     for (int code = 0; code < 200; code++) {
         const int t2 = code / 25, x = (code / 5) % 5, y = code % 5;
+        if (mfe) {   // energies: the inverse factor is the negated mismatch
+            const int mm = t2 ? P.mmI[t2][x][y] : 0;
+            ct[CT_INVMM + code] = t2 ? static_cast<float>(-mm) : MFE_BIG;
+            ct[CT_BUL + code] = t2 ? static_cast<float>(-mm + (t2 > 2 ? P.TermAU : 0)) : MFE_BIG;
+            ct[CT_ONEN + code] = t2 ? static_cast<float>(-mm + P.mm1nI[t2][x][y]) : MFE_BIG;
+            ct[CT_M23O + code] = t2 ? static_cast<float>(P.mm23I[t2][x][y]) : MFE_BIG;
+            continue;
+        }
         const double mm = t2 ? boltz_d(P.mmI[t2][x][y]) : 0.0;
         const double inv = (mm > 0.0) ? 1.0 / mm : 0.0;
         ct[CT_INVMM + code] = static_cast<float>(inv);
@@ -185,31 +210,29 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
         ct[CT_M23O + code] = static_cast<float>(t2 ? boltz_d(P.mm23I[t2][x][y]) : 0.0);
     }
     for (int a = 0; a < 8; a++)
-        for (int b = 0; b < 8; b++) ct[CT_STK + a * 8 + b] = (a && b) ? boltz(P.stack[a][b]) : 0.f;
+        for (int b = 0; b < 8; b++) ct[CT_STK + a * 8 + b] = (a && b) ? F(P.stack[a][b]) : F.zero();
     for (int u = 0; u < 32; u++) {
         const int uu = std::min(u, MAXLOOP);
-        ct[CT_FB + u] = static_cast<float>(boltz_d(P.bulge[uu]) * sp(u + 2));
+        ct[CT_FB + u] = F(P.bulge[uu], u + 2);
         const int nl = u;
         const double e1n = (nl >= 1 && nl + 1 <= MAXLOOP)
                                ? P.interior[nl + 1] + std::min(P.maxninio, (nl - 1) * P.ninio)
                                : INF_E;
-        ct[CT_F1N + u] = static_cast<float>(boltz_d(e1n) * sp(nl + 3));
+        ct[CT_F1N + u] = F(e1n, nl + 3);
     }
-    ct[CT_FSM + 0] = static_cast<float>(sp(2));
-    ct[CT_FSM + 1] = static_cast<float>(boltz_d(P.bulge[1]) * sp(3));
-    ct[CT_FSM + 2] = static_cast<float>(sp(4));
-    ct[CT_FSM + 3] = static_cast<float>(sp(5));
-    ct[CT_FSM + 4] = static_cast<float>(sp(6));
-    ct[CT_FSM + 5] = static_cast<float>(boltz_d(P.interior[5] + P.ninio) * sp(7));
-    ct[CT_FSM + 6] = static_cast<float>(boltz_d(P.TermAU));
-    ct[CT_ONE] = 1.f;
+    ct[CT_FSM + 0] = F(0, 2);
+    ct[CT_FSM + 1] = F(P.bulge[1], 3);
+    ct[CT_FSM + 2] = F(0, 4);
+    ct[CT_FSM + 3] = F(0, 5);
+    ct[CT_FSM + 4] = F(0, 6);
+    ct[CT_FSM + 5] = F(P.interior[5] + P.ninio, 7);
+    ct[CT_FSM + 6] = F(P.TermAU);
+    ct[CT_ONE] = F.one();
     for (int u = 6; u <= MAXLOOP; u++)
         for (int n1 = 2; n1 < 2 + FG_ROW; n1++) {
             const int n2 = u - n1;
-            double f = 0.0;
-            if (n2 >= 2)
-                f = boltz_d(P.interior[u] + std::min(P.maxninio, std::abs(n1 - n2) * P.ninio)) * sp(u + 2);
-            X.fgen[(u - 6) * FG_ROW + n1 - 2] = static_cast<float>(f);
+            X.fgen[(u - 6) * FG_ROW + n1 - 2] =
+                n2 >= 2 ? F(P.interior[u] + std::min(P.maxninio, std::abs(n1 - n2) * P.ninio), u + 2) : F.zero();
         }
     // term lists ordered by u (dev_types.hpp NS_MAX)
     int ns = 0, ng = 0;
@@ -240,15 +263,21 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
     }
     X.s_cnt[31] = ns;
     X.g_cnt[31] = ng;
-    for (int k = 0; k < NMAX + 4; k++) X.sig[k] = static_cast<float>(sp(k));
+    for (int k = 0; k < NMAX + 4; k++) X.sig[k] = F(0, k);
     for (int u = 0; u <= NMAX; u++) {
-        double e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + P.lxc * std::log(u / 30.0);
-        X.hp[u] = static_cast<float>(boltz_d(e) * sp(u + 2));
+        if (mfe) {   // the MFE truncates the long-loop extrapolation to dcal (oracle E_hairpin_int)
+            const int e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + static_cast<int>(P.lxc * std::log(u / 30.0));
+            X.hp[u] = F(e);
+        } else {
+            const double e = (u <= 30) ? P.hairpin[u] : P.hairpin[30] + P.lxc * std::log(u / 30.0);
+            X.hp[u] = F(e, u + 2);
+        }
     }
     const double mlb = boltz_d(P.MLbase);
-    for (int t = 0; t <= NMAX; t++) X.pwml[t] = static_cast<float>(std::pow(mlb * sigma, t));
-    X.mlclosing = static_cast<float>(boltz_d(P.MLclosing) * sp(2));
-    X.mlbase_sig = static_cast<float>(mlb * sigma);
+    for (int t = 0; t <= NMAX; t++)
+        X.pwml[t] = mfe ? static_cast<float>(t * P.MLbase) : static_cast<float>(std::pow(mlb * sigma, t));
+    X.mlclosing = F(P.MLclosing, 2);
+    X.mlbase_sig = F(P.MLbase, 1);
     int nsp = 0;
     auto add_special = [&](const std::vector<std::pair<std::string, int>> &tab) {
         for (auto &e : tab) {
@@ -256,7 +285,7 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
             std::vector<uint8_t> codes(e.first.size());
             for (size_t k = 0; k < e.first.size(); k++) codes[k] = static_cast<uint8_t>(base_code(e.first[k]));
             X.sp_key[nsp] = hp_key(codes.data(), 0, static_cast<int>(codes.size()));
-            X.sp_val[nsp] = static_cast<float>(boltz_d(e.second) * sp(static_cast<int>(codes.size())));
+            X.sp_val[nsp] = F(e.second, static_cast<int>(codes.size()));
             nsp++;
         }
     };
@@ -264,7 +293,7 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
     add_special(P.tetraloops);
     add_special(P.hexaloops);
     X.n_special = nsp;
-    X.log_sigma = std::log(sigma);
+    X.log_sigma = mfe ? 0.0 : std::log(sigma);
     X.kT = kT_kcal();
     if (m.present) {
         const int L = static_cast<int>(m.seq.size());
@@ -274,8 +303,12 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
             X.motif_pt[k] = static_cast<int8_t>(mpt[k]);
         }
         const double beff = (m.mode == ADX_MOTIF_REPLACE) ? m.energy_kcal - eint : m.energy_kcal;
-        const double extra = boltz_d(eint * 100.0) * (boltz_d(beff * 100.0) - 1.0) * sp(L);
-        X.motif_extra = static_cast<float>(extra);
+        if (mfe) {   // min-plus image of the extra term: the formed motif's energy, rounded once to dcal
+            X.motif_extra = static_cast<float>(std::lround(100.0 * (eint + beff)));
+        } else {
+            const double extra = boltz_d(eint * 100.0) * (boltz_d(beff * 100.0) - 1.0) * sp(L);
+            X.motif_extra = static_cast<float>(extra);
+        }
     }
 }
 
@@ -367,6 +400,7 @@ struct Problem {
     std::vector<DevTermMap> tmap;
     int n_terms = 0, n_ctx_eff = 1;
     bool qbm = true;
+    int mode = 0;                // 0 = partition functions, 1 = MFE (ADX_FOLD_*)
     DevBuf<DevTables> dT;
     DevBuf<DevScaled> dX;
     DevBuf<DevVariant> dV;
@@ -414,6 +448,8 @@ struct Problem {
         ka.cells = Nmax >= 5 ? (Nmax - 4) * (Nmax - 3) / 2 : 1;
         ka.groups2 = dGroups2.p;
         ka.n_groups2 = static_cast<int>(groups2.size() / 2);
+        ka.opt = 0;
+        ka.mode = mode;
         return ka;
     }
 
@@ -432,7 +468,7 @@ struct Problem {
     }
 
     adx_status upload_scaled() {
-        build_scaled(*P, sigma(), motif, motif_eint, motif_pt, *hX);
+        build_scaled(*P, sigma(), motif, motif_eint, motif_pt, *hX, mode == 1);
         HIP_TRY(dX.upload(hX.get(), 1, stream));
         return ADX_OK;
     }
@@ -440,7 +476,7 @@ struct Problem {
     adx_status upload_all() {
         hT = std::make_unique<DevTables>();
         hX = std::make_unique<DevScaled>();
-        build_tables(*P, *hT);
+        build_tables(*P, *hT, mode == 1);
         HIP_TRY(dT.upload(hT.get(), 1, stream));
         adx_status s = upload_scaled();
         if (s) return s;
@@ -558,9 +594,10 @@ extern "C" adx_status adx_fold_add_constraint(adx_fold *f, const char *db) {
     return ADX_OK;
 }
 
-extern "C" adx_status adx_fold_pf(adx_fold *f, float *energy) {
-    if (!f || !energy) return fail(ADX_EINVAL, "adx_fold_pf: null argument");
+// One fold of the compound f in mode 0 (partition function) or 1 (MFE).
+static adx_status fold_energy(adx_fold *f, int mode, float *energy) {
     Problem pb;
+    pb.mode = mode;
     pb.device = f->device;
     pb.P = &f->params->P;
     adx_status s = pb.init_device();
@@ -592,6 +629,14 @@ extern "C" adx_status adx_fold_pf(adx_fold *f, float *energy) {
     HIP_TRY(dsc.alloc(1));
     HIP_TRY(ddg.alloc(1));
     float g = NAN;
+    if (mode == 1) {   // integer min-plus: no scale to calibrate
+        s = pb.score(dseq.p, 1, dsc.p, nullptr, ddg.p);
+        if (s) return s;
+        HIP_TRY(hipMemcpyAsync(&g, ddg.p, sizeof(float), hipMemcpyDeviceToHost, pb.stream));
+        HIP_TRY(hipStreamSynchronize(pb.stream));
+        *energy = g;
+        return ADX_OK;
+    }
     for (int attempt = 0; attempt < 6; attempt++) {
         s = pb.score(dseq.p, 1, dsc.p, nullptr, ddg.p);
         if (s) return s;
@@ -613,6 +658,16 @@ extern "C" adx_status adx_fold_pf(adx_fold *f, float *energy) {
     }
     *energy = g;
     return ADX_OK;
+}
+
+extern "C" adx_status adx_fold_pf(adx_fold *f, float *energy) {
+    if (!f || !energy) return fail(ADX_EINVAL, "adx_fold_pf: null argument");
+    return fold_energy(f, 0, energy);
+}
+
+extern "C" adx_status adx_fold_mfe(adx_fold *f, float *energy) {
+    if (!f || !energy) return fail(ADX_EINVAL, "adx_fold_mfe: null argument");
+    return fold_energy(f, 1, energy);
 }
 
 extern "C" adx_status adx_fold_bpp(adx_fold *f, int i, int j, double *prob) {
@@ -734,6 +789,8 @@ extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
         if (T.condition != ADX_APO && T.condition != ADX_HOLO) return fail(ADX_EINVAL, "bad condition");
         c->terms.push_back(T);
     }
+    if (d->fold_mode != ADX_FOLD_PF && d->fold_mode != ADX_FOLD_MFE) return fail(ADX_EINVAL, "bad fold_mode");
+    pb.mode = d->fold_mode;
     c->thermo = d->thermostat;
     if (c->thermo.kind == ADX_THERMO_ANNEAL && c->thermo.cycle_len <= 0)
         return fail(ADX_EINVAL, "annealing cycle length must be positive");
@@ -837,8 +894,10 @@ extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
     if (c->clo_pos.empty()) { c->clo_pos.push_back(0); c->clo_par.push_back(0); }
     s = pb.upload_all();
     if (s) return s;
-    s = calibrate(pb, encode(c->templ));
-    if (s) return s;
+    if (pb.mode == ADX_FOLD_PF) {   // the MFE tables carry no scale
+        s = calibrate(pb, encode(c->templ));
+        if (s) return s;
+    }
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
     HIP_TRY(c->d_mut.upload(c->mut.data(), c->mut.size(), pb.stream));

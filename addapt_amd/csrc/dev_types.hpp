@@ -51,7 +51,15 @@ constexpr int NS_MAX = 128;
 constexpr int NG_MAX = 384;
 enum TermKind : uint8_t { TK_STK = 0, TK_B1, TK_I11, TK_I12, TK_I21, TK_I22, TK_M23, TK_BUL, TK_1N };
 
-struct DevTables {         // exp(-E/kT), FP32; pair type 0 rows are 0
+// Fold modes.  Partition function (KArgs::mode 0): DevTables / DevScaled hold
+// FP32 Boltzmann factors (with the pf scale sigma^k), "impossible" = 0.
+// Minimum free energy (mode 1): the same layouts hold energies in dcal/mol
+// (integers, exact in FP32), factor products become sums, sigma^k becomes 0,
+// "impossible" = MFE_BIG (kernels.hip MinPlus).
+constexpr float MFE_BIG = 1.0e7f;
+constexpr float MFE_MARK = 3.0e7f;   // non-pairable cell mark of the MFE tables
+
+struct DevTables {         // exp(-E/kT) (PF) or E (MFE), FP32; pair type 0 rows are "impossible"
     float stack[8][8];
     float mmH[8][5][5];
     float mmI[8][5][5];
@@ -130,6 +138,7 @@ struct KArgs {
     const int *groups2;         // [n_groups2][2]: variants folded in lockstep (apo, holo of one
     int n_groups2;              //   (context, macrostate); a lone variant is paired with itself)
     int opt;                    // launch-time LDS options (kernels.hip choose_opt)
+    int mode;                   // 0 = partition functions, 1 = minimum free energies (MinPlus tables)
 };
 
 // Monte Carlo state (device, read/write).

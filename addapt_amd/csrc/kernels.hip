@@ -48,28 +48,64 @@ __device__ __forceinline__ int off(int dd, int N) { return ((dd - 4) * (2 * N - 
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Full-wave sum via DPP (quad_perm, row_shr, row_bcast): VALU-only, no LDS
-// crossbar; the total lands in lane 63 and is read back with readlane.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_add(float v) {
-    const int moved = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false);
-    return v + __int_as_float(moved);
+// ---------------------------------------------------------------- semirings
+// One kernel body folds both energy models:
+//   SumProd  McCaskill partition function: FP32 Boltzmann factors with the pf
+//            scale sigma (vrna_pf);
+//   MinPlus  Zuker minimum free energy: integer dcal/mol held in FP32 (exact
+//            below 2^24), "impossible" = BIG and above (never +inf, so 0/1
+//            selector products stay finite), the same loop decomposition with
+//            sums of energies in place of products of factors.
+// The non-pairable cell mark (a value a finished cell never takes) is -0.0f
+// for SumProd and MARK for MinPlus.
+struct SumProd {
+    static constexpr bool MFE = false;
+    __device__ static float zero() { return 0.f; }
+    __device__ static float one() { return 1.f; }
+    __device__ static float add(float a, float b) { return a + b; }
+    __device__ static float mul(float a, float b) { return a * b; }
+    __device__ static float fma(float a, float b, float c) { return fmaf(a, b, c); }
+    __device__ static float mark() { return -0.0f; }
+    __device__ static bool is_mark(float x) { return __float_as_uint(x) == 0x80000000u; }
+    __device__ static float fin(float x) { return x + 0.0f; }   // never -0
+};
+struct MinPlus {
+    static constexpr bool MFE = true;
+    __device__ static float zero() { return MFE_BIG; }
+    __device__ static float one() { return 0.f; }
+    __device__ static float add(float a, float b) { return fminf(a, b); }
+    __device__ static float mul(float a, float b) { return a + b; }
+    __device__ static float fma(float a, float b, float c) { return fminf(a + b, c); }
+    __device__ static float mark() { return MFE_MARK; }
+    __device__ static bool is_mark(float x) { return x == MFE_MARK; }
+    __device__ static float fin(float x) { return fminf(x, MFE_BIG); }   // never MARK
+};
+
+// Full-wave reductions via DPP (quad_perm, row_shr, row_bcast): VALU-only, no
+// LDS crossbar.  Lanes a DPP move does not write keep the identity (SR::zero).
+template <class SR, int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_op(float v) {
+    const int moved = __builtin_amdgcn_update_dpp(__float_as_int(SR::zero()), __float_as_int(v), CTRL, ROWS,
+                                                  0xf, false);
+    return SR::add(v, __int_as_float(moved));
 }
-// Sum over each row of 16 lanes; the row total lands in lane 15 of the row.
+// Reduction over each row of 16 lanes; the row total lands in lane 15 of the row.
+template <class SR = SumProd>
 __device__ __forceinline__ float row_sum(float v) {
-    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
-    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
+    v = dpp_op<SR, 0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_op<SR, 0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_op<SR, 0x114, 0xf>(v);  // row_shr:4
+    v = dpp_op<SR, 0x118, 0xf>(v);  // row_shr:8
     return v;
 }
+template <class SR = SumProd>
 __device__ __forceinline__ float wave_sum(float v) {
-    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
-    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
-    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15
-    v = dpp_add<0x143, 0xc>(v);  // row_bcast:31
+    v = dpp_op<SR, 0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_op<SR, 0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_op<SR, 0x114, 0xf>(v);  // row_shr:4
+    v = dpp_op<SR, 0x118, 0xf>(v);  // row_shr:8
+    v = dpp_op<SR, 0x142, 0xa>(v);  // row_bcast:15
+    v = dpp_op<SR, 0x143, 0xc>(v);  // row_bcast:31
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
@@ -245,30 +281,31 @@ __device__ __forceinline__ int cdiv_pos(int x, int y) {
 }
 __device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-// Sums of two per-lane values over the wave: permlane32 swap folds the halves
-// (lanes 0-31 then carry a, 32-63 carry b), one row/half DPP chain finishes.
+// Reductions of two per-lane values over the wave: permlane32 swap folds the
+// halves (lanes 0-31 then carry a, 32-63 carry b), one row/half DPP chain finishes.
+template <class SR>
 __device__ __forceinline__ void wave_sum2(float a, float b, float &sa, float &sb) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    v = dpp_add<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-    v = dpp_add<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-    v = dpp_add<0x114, 0xf>(v);  // row_shr:4
-    v = dpp_add<0x118, 0xf>(v);  // row_shr:8
-    v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 -> lane 31 = sum(a), lane 63 = sum(b)
+    float v = SR::add(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    v = dpp_op<SR, 0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v = dpp_op<SR, 0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v = dpp_op<SR, 0x114, 0xf>(v);  // row_shr:4
+    v = dpp_op<SR, 0x118, 0xf>(v);  // row_shr:8
+    v = dpp_op<SR, 0x142, 0xa>(v);  // row_bcast:15 -> lane 31 = red(a), lane 63 = red(b)
     sa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
     sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-template <int P>
+template <class SR, int P>
 __device__ __forceinline__ void wave_sums(const float (&v)[P], float (&s)[P]) {
-    if constexpr (P == 2) wave_sum2(v[0], v[1], s[0], s[1]);
-    else s[0] = wave_sum(v[0]);
+    if constexpr (P == 2) wave_sum2<SR>(v[0], v[1], s[0], s[1]);
+    else s[0] = wave_sum<SR>(v[0]);
 }
 
 // ---------------------------------------------------------------- closing-pair terms
 // Per-lane descriptors of one span's interior-loop terms (lane t of slot s =
 // term s*64 + t of the S / G lists, dev_types.hpp).  Invalid lanes carry offset
-// 0 (a finished cell) and factor 0.
+// 0 (a finished cell) and factor SR::zero().
 struct TermLanes {
     int offG[GSLOTS];      // qbm index of the inner cell minus i
     float fG[GSLOTS];
@@ -291,12 +328,12 @@ struct CellU {
 // Interior-loop sums of (i, j) for the P variants (the outer mismatch of the
 // generic loops applied here): SS / SG slots, MK = constrained cell.  Every
 // loop factor is computed once and applied to the P tables.
-template <int SS, int SG, bool MK, int P>
+template <class SR, int SS, int SG, bool MK, int P>
 __device__ __forceinline__ void qb_terms(const Lds<P> &L, const TermLanes &D, const CellU &u, float gtab,
                                          float (&out)[P]) {
     if (SS == 0) {
 #pragma unroll
-        for (int p = 0; p < P; p++) out[p] = 0.f;
+        for (int p = 0; p < P; p++) out[p] = SR::zero();
         return;
     }
     const float *ct = L.ct;
@@ -324,63 +361,66 @@ __device__ __forceinline__ void qb_terms(const Lds<P> &L, const TermLanes &D, co
         float f = D.fG[s];
         if (MK) {   // constrained cell: n1 <= A and n2 <= B (descriptor re-read from LDS)
             const int pk = L.gd[s * WAVE + lane];
-            f = ((pk & 255) <= u.A && (pk >> 8) <= u.B) ? f : 0.f;
+            f = ((pk & 255) <= u.A && (pk >> 8) <= u.B) ? f : SR::zero();
         }
         fg[s] = f;
     }
-    // slot 0: stack / bulge 1 / 1x1..2x2 tables / 2x3 / bulges / 1xn
+    // slot 0: stack / bulge 1 / 1x1..2x2 tables / 2x3 / bulges / 1xn.  uf and gf
+    // select (0/1 selectors, one per kind) the outer-pair factor and the
+    // prefetched table factor, or the semiring one.
+    const float one = SR::one();
     const int t2 = (c0 * 41) >> 10;
     const int i2 = D.b2 + ((u.ty8 + t2) & D.mwt) + (c0 & D.mwc);
-    const float uf = fmaf(D.eb, u.tau - 1.f, fmaf(D.em, u.mo - 1.f, fmaf(D.e3, u.m23 - 1.f, 1.f)));
-    const float gf = fmaf(D.eg, gtab - 1.f, 1.f);
-    float f0 = ct[D.b1[0] + c0] * ct[i2] * (D.fS[0] * uf) * gf;
+    const float uf = fmaf(D.eb, u.tau - one, fmaf(D.em, u.mo - one, fmaf(D.e3, u.m23 - one, one)));
+    const float gf = fmaf(D.eg, gtab - one, one);
+    float f0 = SR::mul(SR::mul(SR::mul(ct[D.b1[0] + c0], ct[i2]), SR::mul(D.fS[0], uf)), gf);
     if (MK) {
         const int pk = int(L.sd[lane]);
-        f0 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f0 : 0.f;
+        f0 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f0 : SR::zero();
     }
-    float f1 = 0.f;
+    float f1 = SR::zero();
     if (SS > 1) {
         // slot 1: bulges and 1xn only
-        f1 = ct[D.b1[1] + c1] * (D.fS[1] * fmaf(D.em1, u.mo - u.tau, u.tau));
+        f1 = SR::mul(ct[D.b1[1] + c1], SR::mul(D.fS[1], fmaf(D.em1, u.mo - u.tau, u.tau)));
         if (MK) {
             const int pk = int(L.sd[WAVE + lane]);
-            f1 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f1 : 0.f;
+            f1 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f1 : SR::zero();
         }
     }
 #pragma unroll
     for (int p = 0; p < P; p++) {
-        float g0 = 0.f, g1 = 0.f;
+        float g0 = SR::zero(), g1 = SR::zero();
 #pragma unroll
         for (int s = 0; s < SG; s++) {
-            if (s & 1) g1 = fmaf(q[p][s], fg[s], g1);
-            else g0 = fmaf(q[p][s], fg[s], g0);
+            if (s & 1) g1 = SR::fma(q[p][s], fg[s], g1);
+            else g0 = SR::fma(q[p][s], fg[s], g0);
         }
-        float sa = qs0[p] * f0;
-        if (SS > 1) sa = fmaf(qs1[p], f1, sa);
-        out[p] = fmaf(g0 + g1, u.mmo, sa);
+        float sa = SR::mul(qs0[p], f0);
+        if (SS > 1) sa = SR::fma(qs1[p], f1, sa);
+        out[p] = SR::fma(SR::add(g0, g1), u.mmo, sa);
     }
 }
 
-template <bool MK, int P>
+template <class SR, bool MK, int P>
 __device__ __forceinline__ void qb_terms_dispatch(int sS, int sG, const Lds<P> &L, const TermLanes &D,
                                                   const CellU &u, float gtab, float (&out)[P]) {
     if (sS == 2) {
         switch (sG) {
-            case 6: qb_terms<2, 6, MK, P>(L, D, u, gtab, out); return;
-            case 5: qb_terms<2, 5, MK, P>(L, D, u, gtab, out); return;
-            case 4: qb_terms<2, 4, MK, P>(L, D, u, gtab, out); return;
-            case 3: qb_terms<2, 3, MK, P>(L, D, u, gtab, out); return;
-            default: qb_terms<2, 2, MK, P>(L, D, u, gtab, out); return;
+            case 6: qb_terms<SR, 2, 6, MK, P>(L, D, u, gtab, out); return;
+            case 5: qb_terms<SR, 2, 5, MK, P>(L, D, u, gtab, out); return;
+            case 4: qb_terms<SR, 2, 4, MK, P>(L, D, u, gtab, out); return;
+            case 3: qb_terms<SR, 2, 3, MK, P>(L, D, u, gtab, out); return;
+            default: qb_terms<SR, 2, 2, MK, P>(L, D, u, gtab, out); return;
         }
     }
     if (sS == 1) {
         switch (sG) {
-            case 0: qb_terms<1, 0, MK, P>(L, D, u, gtab, out); return;
-            case 1: qb_terms<1, 1, MK, P>(L, D, u, gtab, out); return;
-            default: qb_terms<1, 2, MK, P>(L, D, u, gtab, out); return;
+            case 0: qb_terms<SR, 1, 0, MK, P>(L, D, u, gtab, out); return;
+            case 1: qb_terms<SR, 1, 1, MK, P>(L, D, u, gtab, out); return;
+            default: qb_terms<SR, 1, 2, MK, P>(L, D, u, gtab, out); return;
         }
     }
-    qb_terms<0, 0, MK, P>(L, D, u, gtab, out);
+    qb_terms<SR, 0, 0, MK, P>(L, D, u, gtab, out);
 }
 
 // ---------------------------------------------------------------- work split
@@ -445,7 +485,7 @@ __device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
 // split sum mla(i+1, j-1) that the qm item of the previous iteration kept.  A qm
 // item is 4 cells x 16 lanes (split points).  Items are cut into NW contiguous
 // ranges of equal estimated cost, one per wave.
-template <int NT, int P>
+template <int NT, int P, class SR>
 __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, const Lds<P> &L,
                          const DevScaled *__restrict__ XS, float (&z)[P]) {
     constexpr int NW = NT / WAVE;
@@ -491,7 +531,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     }
 #pragma unroll
     for (int p = 0; p < P; p++)
-        for (int k = tid; k < 2 * NP; k += NT) L.mla[p][k] = 0.f;
+        for (int k = tid; k < 2 * NP; k += NT) L.mla[p][k] = SR::zero();
     constrained = __syncthreads_or(constrained);
     if (tid == 0) {
         // ViennaRNA's S1 wrap-around (only reaches values that are never used)
@@ -526,8 +566,9 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     if (tid == 0) {
 #pragma unroll
         for (int p = 0; p < P; p++) {
-            L.q5[p][0] = 1.0f;
-            for (int j = 1; j <= 3 && j <= N; j++) L.q5[p][j] = (L.up[j] >= 1) ? L.q5[p][j - 1] * sig1 : 0.f;
+            L.q5[p][0] = SR::one();
+            for (int j = 1; j <= 3 && j <= N; j++)
+                L.q5[p][j] = (L.up[j] >= 1) ? SR::mul(L.q5[p][j - 1], sig1) : SR::zero();
         }
     }
     // cells of every diagonal: wave w takes diagonals 4 + w, 4 + w + NW, ...
@@ -545,26 +586,27 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const int si = L.S[i], sj = L.S[j], sim = L.S[i - 1], sjp = L.S[j + 1];
                 const int type = ptype(si, sj);
                 pr = type != 0 && allowed(L, i, j);
-                float h = 0.f, m1 = 0.f;
+                float h = SR::zero(), m1 = SR::zero();
                 bool mx = false;
                 if (pr) {
                     if (L.up[i + 1] >= u) {
-                        h = -1.f;
+                        bool special = false;
                         if (u == 3 || u == 4 || u == 6) {
                             const uint32_t key = hp_key(L.S, i, u + 2);
                             for (int k = 0; k < nsp; k++)
-                                if (XS->sp_key[k] == key) { h = XS->sp_val[k]; break; }
+                                if (XS->sp_key[k] == key) { h = XS->sp_val[k]; special = true; break; }
                         }
-                        if (h < 0.f)
-                            h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type]
-                                                            : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
+                        if (!special)
+                            h = SR::mul(L.dt[DT_HP + u],
+                                        (u == 3) ? L.dt[DT_TAU + type]
+                                                 : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
                     }
                     mx = dd == mL - 1 && mL > 0 && L.mat[i];
                     m1 = L.dt[DT_MLS + type * 25 + sim * 5 + sjp];
                 }
 #pragma unroll
                 for (int p = 0; p < P; p++) {
-                    L.qbm[p][od + r] = pr ? ((mx && motif[p]) ? h + mextra : h) : -0.0f;
+                    L.qbm[p][od + r] = pr ? ((mx && motif[p]) ? SR::add(h, mextra) : h) : SR::mark();
                     L.qm1[p][colb(j) + i - 1] = m1;
                 }
                 L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
@@ -598,7 +640,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             int base = 0;
             for (int r0 = 0; r0 < c; r0 += WAVE) {
                 const int r = r0 + lane;
-                const bool pr = r < c && __float_as_uint(L.qbm[0][od + r]) != 0x80000000u;
+                const bool pr = r < c && !SR::is_mark(L.qbm[0][od + r]);
                 const unsigned long long bm = __ballot(pr);
                 if (pr) {
                     const int i = r + 1, j = i + dd;
@@ -631,10 +673,11 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     int kb_lo = 0, kb_hi = 0, km_lo = 0, km_hi = 0;
     // closing-pair chunk (lanes = cells of the chunk)
     int ci = 1, cty = 0, cA = 0, cB = 0, cidx = 0, cm1 = 0;
-    float cmmo = 0.f, ctau = 1.f, cmo = 0.f, cm23 = 0.f, cmmc = 0.f, cpm1 = 0.f, cmlc = 0.f, pfx = 0.f;
+    float cmmo = SR::zero(), ctau = SR::one(), cmo = SR::zero(), cm23 = SR::zero(), cmmc = SR::zero();
+    float cpm1 = SR::zero(), cmlc = SR::zero(), pfx = SR::zero();
     float cpre[P];
 #pragma unroll
-    for (int p = 0; p < P; p++) cpre[p] = 0.f;
+    for (int p = 0; p < P; p++) cpre[p] = SR::zero();
     uint8_t *ws = L.wsc + wid * WAVE;
     // term descriptors: offsets advance by k - d per diagonal once every term is
     // valid (d > 36); before that they are recomputed
@@ -677,7 +720,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             int base = 0;
             for (int r0 = 0; r0 < N - d && base < kc + nc; r0 += WAVE) {
                 const int r = r0 + lane;
-                const bool pr = r < N - d && __float_as_uint(L.qbm[0][od + r]) != 0x80000000u;
+                const bool pr = r < N - d && !SR::is_mark(L.qbm[0][od + r]);
                 const unsigned long long m = __ballot(pr);
                 const int rank = base + __popcll(m & ((1ull << lane) - 1ull));
                 if (pr && rank >= kc && rank < kc + nc) ws[rank - kc] = static_cast<uint8_t>(r + 1);
@@ -703,8 +746,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             cA = (wc >> 16) & 255;
             cB = wc >> 24;
             cmmo = L.dt[DT_MMI + oc];
-            ctau = ty > 2 ? eTAU : 1.f;
-            cmo = ct[CT_ONEN + oc] * cmmo;
+            ctau = ty > 2 ? eTAU : SR::one();
+            cmo = SR::mul(ct[CT_ONEN + oc], cmmo);
             cm23 = ct[CT_M23O + oc];
             cidx = od + i - 1;
             cmmc = L.dt[DT_MMI + L.cc[cidx]];
@@ -712,12 +755,12 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             for (int p = 0; p < P; p++) cpre[p] = L.qbm[p][cidx];
             cm1 = colb(j) + i - 1;
             cpm1 = L.qm1[0][cm1];
-            cmlc = mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + sj1 * 5 + si1];
+            cmlc = SR::mul(mlclosing, L.dt[DT_MLS + rtype(ty) * 25 + sj1 * 5 + si1]);
         }
         {   // lane 4c + g: the 1x1 / 1x2 / 2x1 / 2x2 table factor g of cell c (HBM/L2)
             const int c = lane >> 2, g = lane & 3;
             const int n1 = (g >= 2) ? 2 : 1, n2 = (g & 1) ? 2 : 1;
-            pfx = 0.f;
+            pfx = SR::zero();
             if (c < nc && n1 + n2 <= umax) {
                 const int i = wp & 255, j = i + d;
                 const int oc = (wp >> 8) & 255;
@@ -766,7 +809,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const int u = kG[s] - N - 3, n1 = L.gd[t] & 255;
                 const bool ok = t < nG;
                 D.offG[s] = ok ? off(d - 2 - u, N) + n1 : 0;
-                D.fG[s] = ok ? L.gf[t] : 0.f;
+                D.fG[s] = ok ? L.gf[t] : SR::zero();
             }
 #pragma unroll
             for (int s = 0; s < SSLOTS; s++) {
@@ -774,7 +817,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const int u = kS[s] - N - 3, n1 = int(L.sd[t]) & 255;
                 const bool ok = t < nS;
                 D.offS[s] = ok ? off(d - 2 - u, N) + n1 : 0;
-                D.fS[s] = ok ? L.sf[t] : 0.f;
+                D.fS[s] = ok ? L.sf[t] : SR::zero();
             }
         } else {
 #pragma unroll
@@ -801,8 +844,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             const bool upj = d >= 5 && L.up[j] >= 1;
 #pragma unroll
             for (int p = 0; p < P; p++) {
-                cprev[p] = upj ? L.qm1[p][colb(j - 1) + ci - 1] : 0.f;
-                cml[p] = L.mla[p][((d - 2) & 1) * NP + ci + 1] * cmlc;
+                cprev[p] = upj ? L.qm1[p][colb(j - 1) + ci - 1] : SR::zero();
+                cml[p] = SR::mul(L.mla[p][((d - 2) & 1) * NP + ci + 1], cmlc);
             }
         };
         if (kb_lo < kb_hi) late();
@@ -812,7 +855,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         float m1prev[P];
         int m1up = 0;
         if (has1) {
-            m1np = __float_as_uint(L.qbm[0][off(d, N) + i1 - 1]) == 0x80000000u;
+            m1np = SR::is_mark(L.qbm[0][off(d, N) + i1 - 1]);
 #pragma unroll
             for (int p = 0; p < P; p++) m1prev[p] = L.qm1[p][colb(j1 - 1) + i1 - 1];
             m1up = L.up[j1];
@@ -833,7 +876,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const int o1 = colb(jb) + i - 1, orr = rowb(i, N) - 5;
                 float A[P], Pp[P];
 #pragma unroll
-                for (int p = 0; p < P; p++) { A[p] = 0.f; Pp[p] = 0.f; }
+                for (int p = 0; p < P; p++) { A[p] = SR::zero(); Pp[p] = SR::zero(); }
                 int it = 0;
 #ifdef ADX_ABL_QM
                 it = nit;
@@ -843,22 +886,22 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                     const bool ok0 = cell && t0 <= tmax;
                     const bool okr = ok0 && t0 >= 5;
                     const float w0 = L.pw[t0 <= N ? t0 : N];
-                    const float pw0 = (t0 <= upi) ? w0 : 0.f;
+                    const float pw0 = (t0 <= upi) ? w0 : SR::zero();
 #pragma unroll
                     for (int p = 0; p < P; p++) {
                         const float v0 = L.qm1[p][o1 + (ok0 ? t0 : 0)];
                         const float r0 = L.qm[p][orr + (okr ? t0 : 5)];
-                        const float b0 = ok0 ? v0 : 0.f;
-                        A[p] = fmaf(okr ? r0 : 0.f, b0, A[p]);
-                        Pp[p] = fmaf(pw0, b0, Pp[p]);
+                        const float b0 = ok0 ? v0 : SR::zero();
+                        A[p] = SR::fma(okr ? r0 : SR::zero(), b0, A[p]);
+                        Pp[p] = SR::fma(pw0, b0, Pp[p]);
                     }
                 }
 #pragma unroll
                 for (int p = 0; p < P; p++) {
-                    const float sA = row_sum(A[p]);
-                    const float sP = row_sum(Pp[p]);
+                    const float sA = row_sum<SR>(A[p]);
+                    const float sP = row_sum<SR>(Pp[p]);
                     if (l16 == 15 && cell) {
-                        L.qm[p][rowb(i, N) + sq - 4] = sA + sP;
+                        L.qm[p][rowb(i, N) + sq - 4] = SR::add(sA, sP);
                         L.mla[p][(sq & 1) * NP + i] = sA;
                     }
                 }
@@ -875,7 +918,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             }
             float sums[P];
 #pragma unroll
-            for (int p = 0; p < P; p++) sums[p] = 0.f;
+            for (int p = 0; p < P; p++) sums[p] = SR::zero();
             for (int c = 0; c < nc; c++) {
                 CellU u;
                 u.i = __builtin_amdgcn_readlane(ci, c);
@@ -891,22 +934,22 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const float gtab = __shfl(pfx, c * 4 + D.gsel, WAVE);
                 float part[P], tot[P];
 #ifndef ADX_ABL_QBT
-                if (masked) qb_terms_dispatch<true, P>(sS, sG, L, D, u, gtab, part);
-                else qb_terms_dispatch<false, P>(sS, sG, L, D, u, gtab, part);
+                if (masked) qb_terms_dispatch<SR, true, P>(sS, sG, L, D, u, gtab, part);
+                else qb_terms_dispatch<SR, false, P>(sS, sG, L, D, u, gtab, part);
 #else
 #pragma unroll
-                for (int p = 0; p < P; p++) part[p] = gtab * 0.f;
+                for (int p = 0; p < P; p++) part[p] = SR::mul(gtab, SR::zero());
 #endif
-                wave_sums<P>(part, tot);
+                wave_sums<SR, P>(part, tot);
 #pragma unroll
                 for (int p = 0; p < P; p++) sums[p] = (lane == c) ? tot[p] : sums[p];
             }
             if (lane < nc) {
 #pragma unroll
                 for (int p = 0; p < P; p++) {
-                    const float qb = sums[p] + cpre[p] + cml[p];
-                    L.qbm[p][cidx] = qb * cmmc + 0.0f;   // never -0 (the non-pairable mark)
-                    L.qm1[p][cm1] = fmaf(qb, cpm1, cprev[p] * mlbase_sig);
+                    const float qb = SR::add(SR::add(sums[p], cpre[p]), cml[p]);
+                    L.qbm[p][cidx] = SR::fin(SR::mul(qb, cmmc));   // never the non-pairable mark
+                    L.qm1[p][cm1] = SR::fma(qb, cpm1, SR::mul(cprev[p], mlbase_sig));
                 }
             }
         }
@@ -923,7 +966,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             const int sj = L.S[j];
             float acc[P];
 #pragma unroll
-            for (int p = 0; p < P; p++) acc[p] = 0.f;
+            for (int p = 0; p < P; p++) acc[p] = SR::zero();
             for (int q = 0; q < sQ5; q++) {
                 const int k0 = q * WAVE + lane + 1;
                 const bool ok = k0 <= j - 4;
@@ -931,23 +974,23 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const int ix = off(j - k, N) + k - 1;
                 const int ty = ptype(L.S[k], sj);
                 const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? L.S[k - 1] : 5) * 6 + sjp];
-                const float f = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
+                const float f = ok ? SR::mul(ct[CT_INVMM + L.cc[ix]], e) : SR::zero();
 #pragma unroll
-                for (int p = 0; p < P; p++) acc[p] = fmaf(L.q5[p][k - 1] * L.qbm[p][ix], f, acc[p]);
+                for (int p = 0; p < P; p++) acc[p] = SR::fma(SR::mul(L.q5[p][k - 1], L.qbm[p][ix]), f, acc[p]);
             }
             float sum[P];
-            wave_sums<P>(acc, sum);
+            wave_sums<SR, P>(acc, sum);
             if (lane == 0) {
 #pragma unroll
                 for (int p = 0; p < P; p++)
-                    L.q5[p][j] = ((L.up[j] >= 1) ? L.q5[p][j - 1] * sig1 : 0.f) + sum[p];
+                    L.q5[p][j] = SR::add((L.up[j] >= 1) ? SR::mul(L.q5[p][j - 1], sig1) : SR::zero(), sum[p]);
             }
         }
         STAMP(6);
         if (has1 && m1np) {
 #pragma unroll
             for (int p = 0; p < P; p++)
-                L.qm1[p][colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? m1prev[p] * mlbase_sig : 0.f;
+                L.qm1[p][colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? SR::mul(m1prev[p], mlbase_sig) : SR::zero();
         }
         if (d < N) prep(d + 1);
         STAMP(7);
@@ -984,7 +1027,7 @@ __device__ double combine_score(const KArgs &ka, const Lds<P> &L, double *terms_
     return score;
 }
 
-template <int NT, int P>
+template <int NT, int P, class SR>
 __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
                                  const uint8_t *raw, const Lds<P> &L,
                                  float *dG_out, double *terms_out) {
@@ -998,7 +1041,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
             vs[0] = g;
         }
         float z[P];
-        pf_group<NT, P>(ka, vs, raw, L, XS, z);
+        pf_group<NT, P, SR>(ka, vs, raw, L, XS, z);
         if (threadIdx.x == 0) {
 #pragma unroll
             for (int p = 0; p < P; p++) L.G[vs[p]] = static_cast<double>(z[p]);
@@ -1007,10 +1050,13 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
     }
     double s = 0.0;
     if (threadIdx.x == 0) {
-        // ensemble energy -kT (ln Z_scaled - N ln sigma), as vrna_pf (float)
         for (int v = 0; v < ka.n_variants; v++) {
             const int N = ka.variants[v].N;
-            const double g = -XS->kT * (log(L.G[v]) - N * XS->log_sigma);
+            double g;
+            if constexpr (SR::MFE)   // f5[N] in dcal/mol; BIG and above = no structure
+                g = (L.G[v] >= 0.5 * double(MFE_BIG)) ? double(INFINITY) : L.G[v] / 100.0;
+            else                     // ensemble energy -kT (ln Z_scaled - N ln sigma), as vrna_pf (float)
+                g = -XS->kT * (log(L.G[v]) - N * XS->log_sigma);
             L.G[v] = g;
             if (dG_out) dG_out[v] = static_cast<float>(g);
         }
@@ -1019,7 +1065,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
     return s;
 }
 
-template <int NT, int P>
+template <int NT, int P, class SR>
 __global__ void __launch_bounds__(NT, (NT == 768) ? 3 : 4)
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
@@ -1033,7 +1079,7 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
-    const double s = score_sequence<NT, P>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
+    const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
                                           terms ? terms + size_t(w) * nt : nullptr);
     if (threadIdx.x == 0) scores[w] = s;
 }
@@ -1288,13 +1334,13 @@ size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
     return lds_size<1>(ka, pl, rt);
 }
 
-template <int NT, int P>
+template <int NT, int P, class SR>
 static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
                                  float *dG, const int *mask, hipStream_t stream) {
     bool pl, rt;
     choose_opt<P>(ka, pl, rt);
     const size_t lds = lds_size<P>(ka, pl, rt);
-    auto k = score_kernel<NT, P>;
+    auto k = score_kernel<NT, P, SR>;
     static size_t configured = 0;
     if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
@@ -1310,8 +1356,14 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
 
 hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
                           float *dG, const int *mask, hipStream_t stream) {
-    if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2>(ka, seqs, W, scores, terms, dG, mask, stream);
-    return launch_score_t<512, 1>(ka, seqs, W, scores, terms, dG, mask, stream);
+    // ka.mode: 0 = partition functions (vrna_pf), 1 = minimum free energies
+    if (ka.mode == 1) {
+        if (choose_p(ka) == 2)
+            return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+        return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+    }
+    if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
+    return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
 }
 
 hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, double *scores,

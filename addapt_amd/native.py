@@ -18,6 +18,7 @@ OK, EINVAL, EHIP, ECONSTRAINT, EPARAM, ENOMEM, EMOVE, ESTATE, ENODEV, EUNSUPPORT
 APO, HOLO = 0, 1
 THERMO_FIXED, THERMO_ANNEAL, THERMO_AUTO = 0, 1, 2
 MOTIF_ADD, MOTIF_REPLACE = 0, 1
+FOLD_PF, FOLD_MFE = 0, 1
 OUTCOMES = ["REJECT", "ACCEPT_WORSENED", "ACCEPT_UNCHANGED", "ACCEPT_IMPROVED"]
 
 
@@ -49,7 +50,7 @@ class RunDesc(C.Structure):
                 ("aptamer_fold", C.c_char_p), ("aptamer_energy_kcal", C.c_double),
                 ("motif_mode", C.c_int), ("n_contexts", C.c_int),
                 ("contexts", C.POINTER(ContextDesc)), ("thermostat", Thermostat),
-                ("device", C.c_int)]
+                ("device", C.c_int), ("fold_mode", C.c_int)]
 
 
 class Info(C.Structure):
@@ -68,7 +69,7 @@ class Trace(C.Structure):
 EXPORTS = [
     "adx_last_error", "adx_abi_version", "adx_params_load", "adx_params_free", "adx_kT",
     "adx_eval_structure", "adx_fold_create", "adx_fold_add_motif", "adx_fold_add_constraint",
-    "adx_fold_pf", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
+    "adx_fold_pf", "adx_fold_mfe", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
     "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
     "adx_walkers_import", "adx_set_temperature",
@@ -94,6 +95,7 @@ def lib():
         L.adx_fold_add_motif.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_double]
         L.adx_fold_add_constraint.argtypes = [C.c_void_p, C.c_char_p]
         L.adx_fold_pf.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
+        L.adx_fold_mfe.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
         L.adx_fold_bpp.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
         L.adx_fold_free.argtypes = [C.c_void_p]
         L.adx_ctx_create.argtypes = [C.POINTER(RunDesc), C.POINTER(C.c_void_p)]
@@ -180,6 +182,11 @@ class Fold:
         _check(lib().adx_fold_pf(self.ptr, C.byref(g)))
         return g.value
 
+    def mfe(self):
+        g = C.c_float()
+        _check(lib().adx_fold_mfe(self.ptr, C.byref(g)))
+        return g.value
+
     def bpp(self, i, j):
         p = C.c_double()
         _check(lib().adx_fold_bpp(self.ptr, i, j, C.byref(p)))
@@ -205,10 +212,11 @@ class Engine:
 
     terms: list of (condition 'apo'|'holo', macrostate index, favorable bool, weight)
     aptamer: None or (seq, fold, energy_kcal); contexts: list of (before, after).
+    fold_mode: "pf" (ensembles, vrna_pf) or "mfe" (minimum free energies, ADX_FOLD_MFE).
     """
 
     def __init__(self, sequence, macrostates, terms, aptamer=None, thermostat=None, contexts=None,
-                 motif_mode=MOTIF_ADD, params=None, device=0):
+                 motif_mode=MOTIF_ADD, params=None, device=0, fold_mode="pf"):
         self.params = params or default_params()
         self.N = len(sequence)
         d = RunDesc()
@@ -233,6 +241,8 @@ class Engine:
         d.contexts = self._ctx
         d.thermostat = thermostat if thermostat is not None else make_thermostat()
         d.device = device
+        d.fold_mode = {"pf": FOLD_PF, "mfe": FOLD_MFE}[fold_mode]
+        self.fold_mode = fold_mode
         self._desc = d
         self.ptr = C.c_void_p()
         _check(lib().adx_ctx_create(C.byref(d), C.byref(self.ptr)))

@@ -10,6 +10,9 @@ FLOPs per partition function (DESIGN.md "Roofline"):
                             for every cell (i,j) with 4 <= j-i <= N-6.
 Exterior, hairpin and O(1)-per-cell work are not counted.  Pure numpy, no
 oracle (the product may not call the checker).
+
+The MFE (min-plus) pass visits the same terms: 2 ops per interior term
+(c[p][q] + E, min) and 2 per multiloop / split term (add, min).
 """
 import numpy as np
 
@@ -95,3 +98,8 @@ def pf_terms(seq, cst=None):
 def pf_flops(seq, cst=None):
     a, b = pf_terms(seq, cst)
     return 3 * a + 2 * b
+
+
+def mfe_ops(seq, cst=None):
+    a, b = pf_terms(seq, cst)
+    return 2 * a + 2 * b

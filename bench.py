@@ -3,11 +3,17 @@
 
 A "step" is one MonteCarlo::apply iteration (sampling.cc:55-99) for every
 walker of the batch: thermostat, mutation move, and -- when the sequence
-changed -- the default objective's 4 McCaskill partition functions
-(apo/holo x unconstrained/"active", scoring.cc:145-146, 58, 65) and the
-Metropolis test.  ACCEPT_UNCHANGED steps count, as in the reference counters.
+changed -- the default objective's 4 folds (apo/holo x unconstrained/"active",
+scoring.cc:145-146, 58, 65) and the Metropolis test.  ACCEPT_UNCHANGED steps
+count, as in the reference counters.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 4096] [--length 100]
+--fold mfe (default): BASELINE.json configs[1], the configuration the metric is
+quoted on -- "4096 independent walkers, 100-nt, MFE-fold score only": the 4
+folds are minimum free energies (ADX_FOLD_MFE).
+--fold pf: the same objective over McCaskill partition functions (vrna_pf, the
+reference's own scoring path; config 3 without the bppm term).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 4096] [--length 100] [--fold mfe|pf]
 
 N > 1: launched by torch.distributed.run, one rank per GPU; walkers are
 sharded (weak scaling, global walker id = rank * W + w), no collective on
@@ -35,25 +41,28 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--walkers", type=int, default=4096)
     ap.add_argument("--length", type=int, default=100)
+    ap.add_argument("--fold", choices=("mfe", "pf"), default="mfe",
+                    help="mfe = BASELINE configs[1] (default); pf = partition-function objective")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="approximate budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--replica-interval", type=int, default=0,
                     help="BASELINE config 5: one temperature rung per rank (0.5*1.5^r), RCCL swap of "
                          "walker configurations between neighbouring rungs every K steps (N > 1 only)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic "
+                         "(default profiles/traffic_latest_<fold>.json)")
     return ap.parse_args()
 
 
-def cpu_baseline(tmpl, active, walker_seqs, budget_s):
+def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold):
     """Oracle MC (the C++-equivalent CPU restatement, 'port') on the host cores."""
     from oracle import oracle as O
     from addapt_amd import workloads
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
-    sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
+    sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif, mode=fold)
     th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     # probe: 1 walker x 4 steps on one thread to size the sample
     t_probe, _ = O.mc_run_batch(sf, walker_seqs[:1], [active], th, [0], 4, 1)
@@ -67,8 +76,9 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s):
     total = walkers * steps
     return {"value": total / t, "unit": "MC steps/s", "cores": threads, "kind": "port",
             "sample": "%d walkers x %d steps of the same workload (oracle/ C restatement of "
-                      "MonteCarlo::apply + ViennaRNA pf, FP64, 1 walker per OpenMP thread), %.1f s"
-                      % (walkers, steps, t),
+                      "MonteCarlo::apply + %s, 1 walker per OpenMP thread), %.1f s"
+                      % (walkers, steps, "ViennaRNA-style pf, FP64" if fold == "pf"
+                         else "integer-dcal MFE", t),
             "per_core": total / t / threads,
             "reference_2016_per_core": 14.4}
 
@@ -100,7 +110,8 @@ def main():
         th = native.make_thermostat("fixed", t=temps[rank])
     else:
         th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
-    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank)
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank,
+                        fold_mode=a.fold)
     W = a.walkers
     gids = shard.walker_ids(rank, world, W)
     seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + gids[0])
@@ -137,12 +148,15 @@ def main():
     scored = int(dc[:, 0].sum() + dc[:, 1].sum() + dc[:, 3].sum())
     outcomes = shard.sum_over_ranks(dc.sum(axis=0), dist, device="cuda" if dist is not None else None)
     sample = [tmpl] + seqs[:7]
-    f_free = sum(roofline.pf_flops(s, None) for s in sample) / len(sample)
-    f_act = sum(roofline.pf_flops(s, active) for s in sample) / len(sample)
+    work = roofline.pf_flops if a.fold == "pf" else roofline.mfe_ops
+    f_free = sum(work(s, None) for s in sample) / len(sample)
+    f_act = sum(work(s, active) for s in sample) / len(sample)
     flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
     launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
     achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
     traffic, traffic_src = None, None
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_latest_%s.json" % a.fold)
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             tj = json.load(f)
@@ -155,9 +169,12 @@ def main():
         "unit": "TFLOP/s",
         "frac": (achieved_tflops / FP32_PEAK_TFLOPS) if achieved_tflops else None,
         "traffic": traffic,
-        "compute_unit": "fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
-                        "products, not a contraction); peak = gfx950 fp32 rate, vector == matrix",
-        "kernel": "score_kernel<512>",
+        "compute_unit": ("fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
+                         "products, not a contraction); peak = gfx950 fp32 rate, vector == matrix")
+        if a.fold == "pf" else
+        ("fp32 VALU add/min on integer dcal energies (min-plus is not an MFMA contraction); "
+         "peak = gfx950 fp32 rate"),
+        "kernel": "score_kernel<%s>" % ("MinPlus" if a.fold == "mfe" else "SumProd"),
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": score_ms,
         "launches": launches,
@@ -180,13 +197,17 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32",   # MFE: integer dcal/mol values, exact in fp32 add/min
         "data": "synthetic",
         "config": {
-            "workload": "default objective (apo: not active, holo: active; THEO aptamer 0.32 uM): "
-                        "4 McCaskill inside PFs per scored step, synthetic %d-nt sgRNA template "
+            "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
+                        "0.32 uM), 4 %s per scored step, synthetic %d-nt sgRNA template "
                         "(SURVEY.md 8d), %d walkers per GPU, annealing 5 to 0 in 300 steps"
-                        % (a.length, W),
+                        % ("BASELINE configs[1] (MFE-fold score only)" if a.fold == "mfe"
+                           else "partition-function score (config 3 without bppm)",
+                           "minimum-free-energy folds" if a.fold == "mfe" else "McCaskill inside PFs",
+                           a.length, W),
+            "fold": a.fold,
             "walkers_per_gpu": W,
             "global_walkers": W * world,
             "length": a.length,
@@ -198,7 +219,7 @@ def main():
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds, a.fold)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

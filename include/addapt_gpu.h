@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ADX_ABI_VERSION 1
+#define ADX_ABI_VERSION 2
 
 typedef enum adx_status {
     ADX_OK = 0,
@@ -75,6 +75,12 @@ adx_status adx_fold_add_motif(adx_fold *f, const char *motif_seq, const char *mo
 adx_status adx_fold_add_constraint(adx_fold *f, const char *dot_bracket);
 /* vrna_pf(fc, NULL) (:58, :65): ensemble free energy (kcal/mol, float) */
 adx_status adx_fold_pf(adx_fold *f, float *energy_kcal);
+/* vrna_mfe(fc, NULL) (fold.h, included at scoring.cc:9, never called by the
+ * reference): minimum free energy (kcal/mol, float; integer dcal arithmetic;
+ * +inf when the constraint admits no structure), with the ligand motif
+ * entering as c(i,j) = min(c(i,j), round(100*(E_motif + bonus))) at every site
+ * where the motif can form.  Energy only, no structure. */
+adx_status adx_fold_mfe(adx_fold *f, float *energy_kcal);
 /* fc->exp_matrices->probs[fc->iindx[i] - j] with 1-based i < j (:47-50);
  * computed on first use with md.compute_bpp (:41-44). */
 adx_status adx_fold_bpp(adx_fold *f, int i, int j, double *prob);
@@ -111,6 +117,10 @@ typedef struct adx_thermostat {
 #define ADX_MOTIF_ADD 0        /* ligand bonus added to the motif structure */
 #define ADX_MOTIF_REPLACE 1    /* motif structure's total energy := bonus */
 
+#define ADX_FOLD_PF 0          /* MacrostateProbTerm over vrna_pf ensembles (scoring.cc:53-71) */
+#define ADX_FOLD_MFE 1         /* the same terms over minimum free energies:
+                                  p = exp(-(E_mfe(constrained) - E_mfe(free)) / kT) */
+
 typedef struct adx_context_desc { /* Context (model.hh:139-157) */
     const char *before;
     const char *after;
@@ -131,6 +141,7 @@ typedef struct adx_run_desc {
     const adx_context_desc *contexts;
     adx_thermostat thermostat;
     int device;                      /* HIP device ordinal */
+    int fold_mode;                   /* ADX_FOLD_PF (default, zero-initialised) / ADX_FOLD_MFE */
 } adx_run_desc;
 
 typedef struct adx_ctx adx_ctx;

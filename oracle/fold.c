@@ -199,6 +199,7 @@ typedef struct {
     double m_extra; /* Boltzmann extra weight for a formed motif (unscaled) */
     double m_Eint;
     double m_beff;  /* bonus applied to the formed motif (kcal; mode REPLACE: minus Eint) */
+    int m_mfe_dcal; /* motif structure energy incl. bonus for the MFE, lround(100*(Eint+beff)) */
 } model_t;
 
 static int can_pair(const model_t *m, int i, int j) {
@@ -259,6 +260,7 @@ static int model_init(model_t *m, const orc_params *P, const char *seq, const ch
         double beff = motif->mode == 1 ? motif->energy_kcal - eint : motif->energy_kcal;
         m->m_extra = boltz(eint * 100.0) * (boltz(beff * 100.0) - 1.0);
         m->m_beff = beff;
+        m->m_mfe_dcal = (int)lround(100.0 * (eint + beff));
     }
     return 1;
 }
@@ -778,11 +780,12 @@ int orc_mfe(const orc_params *P, const char *seq, const char *constraint, char *
 /* ------------------------------------------------- MFE with the motif */
 /* Minimum free energy (kcal/mol) of the same model the partition function
  * sums over, for the engine's MFE fold mode: the min-plus
- * form of the inside recursion of orc_mfe above, in double so that the
- * ligand motif can enter like it does in the partition function -- a formed
- * motif's closing cell may take the motif structure's energy plus the bonus,
- * c(i,j) = min(c(i,j), Eint + bonus) (the min-plus image of the extra term
- * exp(-Eint)(exp(-bonus) - 1) the PF adds at the same cell). */
+ * form of the inside recursion of orc_mfe above, integer dcal/mol throughout
+ * (held in doubles, every value integral), with the ligand motif entering like
+ * it does in the partition function -- a formed motif's closing cell may take
+ * the motif structure's energy plus the bonus, rounded once to dcal:
+ * c(i,j) = min(c(i,j), lround(100*(Eint + bonus))) (the min-plus image of the
+ * extra term exp(-Eint)(exp(-bonus) - 1) the PF adds at the same cell). */
 double orc_mfe_energy(const orc_params *P, const char *seq, const char *constraint,
                       const orc_motif *motif) {
     model_t m;
@@ -831,8 +834,7 @@ double orc_mfe_energy(const orc_params *P, const char *seq, const char *constrai
                 if (sm < INF && sm + P->MLclosing + E_ml_stem(P, tt, S[j - 1], S[i + 1]) < best)
                     best = sm + P->MLclosing + E_ml_stem(P, tt, S[j - 1], S[i + 1]);
                 if (m.mL && motif_at(&m, i, j)) {
-                    double e = 100.0 * (m.m_Eint + m.m_beff);
-                    if (e < best) best = e;
+                    if (m.m_mfe_dcal < best) best = m.m_mfe_dcal;
                 }
                 c[IDX(i, j)] = best;
             }

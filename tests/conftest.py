@@ -16,8 +16,7 @@ def pytest_configure(config):
 def oracle():
     from oracle import oracle as O
 
-    if not os.path.exists(O.LIB_PATH):
-        O.build()
+    O.build()  # incremental (make): picks up edits to oracle/*.c
     return O
 
 

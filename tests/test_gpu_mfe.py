@@ -1,0 +1,178 @@
+"""GPU parity of the MFE fold mode (BASELINE config 2).
+
+The MFE is integer dcal/mol arithmetic on both sides (oracle/fold.c
+orc_mfe_energy; kernels.hip MinPlus, exact in FP32), so fold energies must be
+BIT-EXACT (float32 equality), including +inf for constraints no structure
+satisfies.  Scores are exp/log of those energies: equal to 1e-12 (the device
+and host libm may differ in the last ulp).  MC trajectories: positions, bases,
+outcomes, thresholds and counters identical.
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from addapt_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_seq(rng, n):
+    return "".join(rng.choice("ACGU") for _ in range(n))
+
+
+def rand_constraint(rng, n, p_x=0.1, n_pairs=2):
+    c = ["."] * n
+    for _ in range(n_pairs):
+        i = rng.randrange(0, n - 8)
+        j = rng.randrange(i + 5, n)
+        if all(ch == "." for ch in c[i:j + 1]):
+            c[i], c[j] = "(", ")"
+    for k in range(n):
+        if c[k] == "." and rng.random() < p_x:
+            c[k] = rng.choice("x|<>") if rng.random() < 0.2 else "x"
+    return "".join(c)
+
+
+def _same(g, ref):
+    ref = np.float32(ref)
+    if math.isinf(ref):
+        return math.isinf(g) and g > 0
+    return np.float32(g) == ref
+
+
+def test_fold_mfe_matches_oracle(native, oracle):
+    rng = random.Random(17)
+    cases = [("GGGAAACCC", None), ("ACGUGAAAACGU", "((((....))))"), ("ACGUGAAAACGU", "xxxx........"),
+             ("AAAAAAAAAA", None), (workloads.THEO_SEQ, None), (workloads.RHF6_SEQ.upper(), None),
+             (workloads.RHF6_SEQ.upper(), workloads.RHF6_ACTIVE)]
+    for n in (20, 37, 64, 100, 150):
+        for _ in range(3):
+            s = rand_seq(rng, n)
+            cases.append((s, None))
+            cases.append((s, rand_constraint(rng, n)))
+    for seq, cst in cases:
+        f = native.Fold(seq)
+        if cst:
+            f.add_constraint(cst)
+        g = f.mfe()
+        ref = oracle.mfe_energy(seq, cst)
+        assert _same(g, ref), (seq, cst, g, ref)
+
+
+def test_fold_mfe_motif(native, oracle):
+    apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
+    e = oracle.theo_bonus()
+    rng = random.Random(5)
+    m = oracle.make_motif(apt, fold, e, 0)
+    for seq in (apt, "GGGA" + apt + "UCCC", rand_seq(rng, 20) + apt + rand_seq(rng, 31),
+                workloads.synthetic(100)[0].upper()):
+        for cst in (None, "." * len(seq)):
+            f = native.Fold(seq)
+            f.add_motif(apt, fold, e)
+            if cst:
+                f.add_constraint(cst)
+            g = f.mfe()
+            assert _same(g, oracle.mfe_energy(seq, cst, m)), (seq, g)
+
+
+def _engine(native, tmpl, macro, terms, thermostat=None, contexts=None):
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    return native.Engine(tmpl, macro, terms, aptamer=apt, contexts=contexts, fold_mode="mfe",
+                         thermostat=thermostat or native.make_thermostat("fixed", t=1.0))
+
+
+def _oracle_sf(oracle, terms, contexts=None):
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts, mode="mfe")
+
+
+def _close(a, b):
+    if math.isinf(b) or math.isnan(b):
+        return (math.isnan(a) and math.isnan(b)) or a == b
+    return abs(a - b) <= 1e-12 * max(1.0, abs(b))
+
+
+@pytest.mark.parametrize("N", [60, 100, 150])
+def test_score_batch_mfe(native, oracle, N):
+    tmpl, active = workloads.synthetic(N)
+    terms = workloads.default_objective()
+    eng = _engine(native, tmpl, [active], terms)
+    seqs = workloads.walker_sequences(tmpl, [active], 24)
+    sc, tv, dg = eng.score_batch(seqs)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(24):
+            ref = oracle.mfe_energy(seqs[w], active if mac >= 0 else None, motif if cond == 1 else None)
+            assert _same(dg[w, v], ref), (N, v, w, dg[w, v], ref)
+    sf = _oracle_sf(oracle, terms)
+    for w in range(24):
+        ref, tref = sf.score(seqs[w], [active])
+        assert _close(sc[w], ref), (w, sc[w], ref)
+        for a, b in zip(tv[w], tref):
+            assert _close(a, b), (w, tv[w], tref)
+
+
+def test_score_batch_mfe_contexts(native, oracle):
+    tmpl, active = workloads.synthetic(80)
+    other = "." * 10 + "(" + "." * 20 + ")" + "." * (80 - 32)
+    terms = [("apo", 0, False, 1.0), ("holo", 0, True, 0.5), ("apo", 1, True, 2.0)]
+    ctx = [("GGAC", "UUA"), ("", "CCCA"), ("AUAUAU", "")]
+    eng = _engine(native, tmpl, [active, other], terms, contexts=ctx)
+    seqs = workloads.walker_sequences(tmpl, [active, other], 6)
+    sc, tv, _ = eng.score_batch(seqs)
+    sf = _oracle_sf(oracle, terms, contexts=ctx)
+    for w in range(6):
+        ref, tref = sf.score(seqs[w], [active, other])
+        assert _close(sc[w], ref), (w, sc[w], ref)
+
+
+def test_mc_trajectory_mfe(native, oracle):
+    tmpl, active = workloads.synthetic(60)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [0, 1, 2, 3, 4, 5, 6, 7]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    steps = 40
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms)
+    for w, seed in enumerate(seeds):
+        # exact energies; only a last-ulp exp() difference at |crit - u| < 1e-12 may be forced
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=1e-12)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert tr["base"][w::len(seeds)] == ref["base"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                assert _close(tr["proposed_score"][s, w], ref["proposed_score"][s]), (w, s)
+                assert tr["random_threshold"][s, w] == ref["random_threshold"][s]
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert _close(scores[w], ref["score"])
+        assert list(counters[w]) == ref["counters"]
+
+
+def test_mc_mfe_full_size_invariants(native, oracle):
+    """Config 2 size (4096 walkers, N=100): counters sum to the steps, every
+    final score equals the oracle's MFE score of the final sequence."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    W = 4096
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(3)
+    final, scores, counters = eng.download()
+    assert (counters.sum(axis=1) == 3).all()
+    sf = _oracle_sf(oracle, terms)
+    for w in list(range(0, W, 257)) + [W - 1]:
+        ref, _ = sf.score(final[w], [active])
+        assert _close(scores[w], ref), (w, scores[w], ref)

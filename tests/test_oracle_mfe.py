@@ -5,7 +5,8 @@ Checks:
 * without a motif it equals the traceback MFE (orc_mfe, already pinned by
   the reference's mfe annotations and by exhaustive enumeration);
 * with a contiguous ADD-mode motif (vrna_sc_add_hi_motif, scoring.cc:92-100)
-  it equals  min(MFE, min_o MFE(seq | motif forced at o) + bonus)  -- the
+  it equals  min(MFE, min_o MFE(seq | motif forced at o) + bonus)  (bonus
+  rounded to dcal/mol: the MFE is integer dcal throughout) -- the
   ligand bonus applies to every structure that contains the motif's pairs
   and unpaired bases at occurrence o (hard constraints: pairs '()' and
   unpaired 'x');
@@ -27,6 +28,10 @@ def test_mfe_energy_matches_traceback(oracle, seq):
     assert oracle.mfe_energy(seq) == pytest.approx(e, abs=1e-9)
 
 
+def _bonus_dcal(oracle):
+    return round(oracle.theo_bonus() * 100) / 100
+
+
 def _motif_forced(seq, o):
     cst = ["."] * len(seq)
     for k, c in enumerate(workloads.THEO_FOLD):
@@ -43,7 +48,7 @@ def test_mfe_with_motif_is_min_over_occurrences(oracle, N):
     assert occ
     expect = oracle.mfe_energy(seq)
     for o in occ:
-        expect = min(expect, oracle.mfe_energy(seq, _motif_forced(seq, o)) + oracle.theo_bonus())
+        expect = min(expect, oracle.mfe_energy(seq, _motif_forced(seq, o)) + _bonus_dcal(oracle))
     assert oracle.mfe_energy(seq, None, m) == pytest.approx(expect, abs=1e-6)
 
 
@@ -52,7 +57,7 @@ def test_mfe_theo_holo(oracle):
     m = oracle.make_motif(seq, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
     e_motif = oracle.eval_structure(seq, workloads.THEO_FOLD)
     assert oracle.mfe_energy(seq, None, m) == pytest.approx(
-        min(oracle.mfe_energy(seq), e_motif + oracle.theo_bonus()), abs=1e-6)
+        min(oracle.mfe_energy(seq), e_motif + _bonus_dcal(oracle)), abs=1e-6)
 
 
 @pytest.mark.parametrize("N", [60, 100])
