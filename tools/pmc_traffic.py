@@ -30,7 +30,7 @@ def main():
     fk = sum(f) / len(f)
     wk = sum(w) / len(w)
     out = {
-        "kernel": "score_kernel<512>",
+        "kernel": "score_kernel",
         "launches": len(f),
         "fetch_size_kb_raw": fk,
         "write_size_kb": wk,
