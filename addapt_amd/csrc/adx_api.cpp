@@ -25,6 +25,9 @@ size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
 hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
                         double *terms, float *dG, hipStream_t stream);
 hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream, hipEvent_t *evs);
+size_t bppm_lds_bytes(const KArgs &ka);
+hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
+                       double *pair_p, hipStream_t stream);
 constexpr int NT = 512;
 constexpr size_t LDS_MAX = 163840;
 }  // namespace adx
@@ -408,6 +411,11 @@ struct Problem {
     DevBuf<int> dCtxOff;
     DevBuf<DevTermMap> dTmap;
     DevBuf<int> dGroups2;
+    // base-pair probability terms: outside variants, requested pairs, per-walker results
+    std::vector<int> bvars;
+    std::vector<int> pairs;      // [n][3]: bvars index, i, j (1-based folded coordinates)
+    DevBuf<int> dBvars, dPairs;
+    DevBuf<double> dPairP;
     std::unique_ptr<DevTables> hT;
     std::unique_ptr<DevScaled> hX;
 
@@ -450,6 +458,11 @@ struct Problem {
         ka.n_groups2 = static_cast<int>(groups2.size() / 2);
         ka.opt = 0;
         ka.mode = mode;
+        ka.bvars = dBvars.p;
+        ka.n_bvars = static_cast<int>(bvars.size());
+        ka.pairs = dPairs.p;
+        ka.n_pairs = static_cast<int>(pairs.size() / 3);
+        ka.pair_p = dPairP.p;
         return ka;
     }
 
@@ -505,12 +518,28 @@ struct Problem {
             groups2.push_back(static_cast<int>(mate));
         }
         HIP_TRY(dGroups2.upload(groups2.data(), groups2.size(), stream));
+        HIP_TRY(dBvars.upload(bvars.data(), bvars.size(), stream));
+        HIP_TRY(dPairs.upload(pairs.data(), pairs.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        if (!pairs.empty() && bppm_lds_bytes(kargs()) == 0)
+            return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", Nmax);
         return choose_layout();
+    }
+
+    // per-walker pair-probability buffer (grow-only)
+    adx_status ensure_pairs(int W) {
+        const size_t need = size_t(W) * (pairs.size() / 3);
+        if (need > 0 && dPairP.n < need) HIP_TRY(dPairP.alloc(need));
+        return ADX_OK;
     }
 
     // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
     adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
+        if (!pairs.empty()) {
+            adx_status s = ensure_pairs(W);
+            if (s) return s;
+            HIP_TRY(launch_bppm(kargs(), dseqs, W, nullptr, nullptr, 0, dPairP.p, stream));
+        }
         HIP_TRY(launch_score(kargs(), qbm, dseqs, W, dscores, dterms, ddG, stream));
         return ADX_OK;
     }
@@ -556,6 +585,7 @@ struct adx_fold {
     int device = 0;
     std::string constraint;  // accumulated (last one wins, like a fresh DB constraint)
     Motif motif;
+    std::vector<double> bpp; // cached N*N probabilities (scoring.cc:41-44 computes them once)
 };
 
 extern "C" adx_status adx_fold_create(const adx_params *p, const char *seq, int with_bppm, int device,
@@ -580,6 +610,7 @@ extern "C" adx_status adx_fold_add_motif(adx_fold *f, const char *mseq, const ch
     f->motif.fold = mfold;
     f->motif.energy_kcal = e;
     f->motif.present = true;
+    f->bpp.clear();
     return ADX_OK;
 }
 
@@ -591,11 +622,12 @@ extern "C" adx_status adx_fold_add_constraint(adx_fold *f, const char *db) {
     adx_status s = build_constraint(db, static_cast<int>(f->seq.size()), tmp);
     if (s) return s;
     f->constraint = db;
+    f->bpp.clear();
     return ADX_OK;
 }
 
 // One fold of the compound f in mode 0 (partition function) or 1 (MFE).
-static adx_status fold_energy(adx_fold *f, int mode, float *energy) {
+static adx_status fold_energy(adx_fold *f, int mode, float *energy, std::vector<double> *bpp = nullptr) {
     Problem pb;
     pb.mode = mode;
     pb.device = f->device;
@@ -657,6 +689,21 @@ static adx_status fold_energy(adx_fold *f, int mode, float *energy) {
         if (s) return s;
     }
     *energy = g;
+    if (bpp) {   // outside pass on the calibrated scale
+        bpp->assign(size_t(N) * N, 0.0);
+        if (!std::isfinite(g)) return ADX_OK;   // empty ensemble: every probability is 0
+        pb.bvars.assign(1, 0);
+        HIP_TRY(pb.dBvars.upload(pb.bvars.data(), 1, pb.stream));
+        const KArgs ka = pb.kargs();
+        if (bppm_lds_bytes(ka) == 0)
+            return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", N);
+        DevBuf<double> dfull;
+        HIP_TRY(dfull.alloc(size_t(N) * N));
+        HIP_TRY(hipMemsetAsync(dfull.p, 0, sizeof(double) * N * N, pb.stream));
+        HIP_TRY(launch_bppm(ka, dseq.p, 1, nullptr, dfull.p, N, nullptr, pb.stream));
+        HIP_TRY(hipMemcpyAsync(bpp->data(), dfull.p, sizeof(double) * N * N, hipMemcpyDeviceToHost, pb.stream));
+        HIP_TRY(hipStreamSynchronize(pb.stream));
+    }
     return ADX_OK;
 }
 
@@ -671,11 +718,19 @@ extern "C" adx_status adx_fold_mfe(adx_fold *f, float *energy) {
 }
 
 extern "C" adx_status adx_fold_bpp(adx_fold *f, int i, int j, double *prob) {
-    (void)i;
-    (void)j;
-    (void)prob;
-    if (!f) return fail(ADX_EINVAL, "adx_fold_bpp: null argument");
-    return fail(ADX_EUNSUPPORTED, "base-pair probabilities (outside pass) are not built yet");
+    if (!f || !prob) return fail(ADX_EINVAL, "adx_fold_bpp: null argument");
+    const int N = static_cast<int>(f->seq.size());
+    if (i < 1 || j < 1 || i > N || j > N) return fail(ADX_EINVAL, "adx_fold_bpp: (%d, %d) outside [1, %d]", i, j, N);
+    if (f->bpp.empty()) {
+        float g = 0.f;
+        adx_status s = fold_energy(f, 0, &g, &f->bpp);
+        if (s) {
+            f->bpp.clear();
+            return s;
+        }
+    }
+    *prob = (i != j) ? f->bpp[size_t(i - 1) * N + (j - 1)] : 0.0;
+    return ADX_OK;
 }
 
 extern "C" void adx_fold_free(adx_fold *f) { delete f; }
@@ -784,8 +839,14 @@ extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
     if (d->n_terms < 0 || d->n_terms > MAX_TERMS) return fail(ADX_EINVAL, "n_terms out of range");
     for (int t = 0; t < d->n_terms; t++) {
         const adx_term &T = d->terms[t];
-        if (T.macrostate < 0 || T.macrostate >= d->n_macrostates)
+        if (T.kind == ADX_TERM_PAIR) {
+            if (T.pair_i < 0 || T.pair_j >= N || T.pair_j - T.pair_i < 1)
+                return fail(ADX_EINVAL, "term %d: pair (%d, %d) outside [0, %d)", t, T.pair_i, T.pair_j, N);
+        } else if (T.kind != ADX_TERM_MACROSTATE) {
+            return fail(ADX_EINVAL, "term %d: bad kind %d", t, T.kind);
+        } else if (T.macrostate < 0 || T.macrostate >= d->n_macrostates) {
             return fail(ADX_EINVAL, "term %d names macrostate %d (have %d)", t, T.macrostate, d->n_macrostates);
+        }
         if (T.condition != ADX_APO && T.condition != ADX_HOLO) return fail(ADX_EINVAL, "bad condition");
         c->terms.push_back(T);
     }
@@ -865,6 +926,24 @@ extern "C" adx_status adx_ctx_create(const adx_run_desc *d, adx_ctx **out) {
     for (int k = 0; k < pb.n_ctx_eff; k++) {
         for (auto &T : c->terms) {
             const int vf = variant(k, T.condition, -1);
+            if (T.kind == ADX_TERM_PAIR) {   // RnaFold::base_pair_prob of the unconstrained fold
+                if (vf < 0) return ADX_ECONSTRAINT;
+                int bv = -1;
+                for (size_t b = 0; b < pb.bvars.size(); b++)
+                    if (pb.bvars[b] == vf) bv = static_cast<int>(b);
+                if (bv < 0) {
+                    bv = static_cast<int>(pb.bvars.size());
+                    pb.bvars.push_back(vf);
+                }
+                const int lb = pb.variants[vf].before_len;
+                const int pidx = static_cast<int>(pb.pairs.size() / 3);
+                pb.pairs.insert(pb.pairs.end(), {bv, T.pair_i + lb + 1, T.pair_j + lb + 1});
+                DevTermMap m{vf, vf, T.favorable, T.weight};
+                m.kind = 1;
+                m.pidx = pidx;
+                pb.tmap.push_back(m);
+                continue;
+            }
             const int vc = variant(k, T.condition, T.macrostate);
             if (vf < 0 || vc < 0) return ADX_ECONSTRAINT;
             pb.tmap.push_back(DevTermMap{vf, vc, T.favorable, T.weight});
@@ -1159,6 +1238,41 @@ extern "C" adx_status adx_set_temperature(adx_ctx *c, double t) {
     if (!c) return fail(ADX_EINVAL, "adx_set_temperature: null context");
     if (c->thermo.kind != ADX_THERMO_FIXED) return fail(ADX_EINVAL, "adx_set_temperature: not a fixed thermostat");
     c->thermo.t_fixed = t;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_bppm_batch(adx_ctx *c, int W, const char *seqs, int condition, int context,
+                                      double *probs) {
+    if (!c || W <= 0 || !seqs || !probs) return fail(ADX_EINVAL, "adx_bppm_batch: bad argument");
+    Problem &pb = c->pb;
+    if (pb.mode != ADX_FOLD_PF) return fail(ADX_EUNSUPPORTED, "adx_bppm_batch: partition-function contexts only");
+    const int want_ctx = c->n_contexts > 0 ? context : -1;
+    int v = -1;
+    for (size_t k = 0; k < pb.variants.size(); k++)
+        if (pb.variants[k].ctx == want_ctx && pb.vmac[k] == -1 && pb.variants[k].motif == (condition == ADX_HOLO ? 1 : 0))
+            v = static_cast<int>(k);
+    if (v < 0) return fail(ADX_EINVAL, "adx_bppm_batch: the objective has no (context %d, condition %d) fold", context, condition);
+    const int N = pb.Nraw, L = pb.variants[v].N;
+    std::vector<uint8_t> codes(size_t(W) * N);
+    for (size_t k = 0; k < codes.size(); k++) codes[k] = static_cast<uint8_t>(base_code(seqs[k]));
+    DevBuf<uint8_t> dseq;
+    DevBuf<int> dbv;
+    DevBuf<double> dfull;
+    HIP_TRY(dseq.upload(codes.data(), codes.size(), pb.stream));
+    HIP_TRY(dbv.upload(&v, 1, pb.stream));
+    KArgs ka = pb.kargs();
+    ka.bvars = dbv.p;
+    ka.n_bvars = 1;
+    ka.n_pairs = 0;
+    ka.pairs = nullptr;
+    ka.pair_p = nullptr;
+    if (bppm_lds_bytes(ka) == 0)
+        return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", pb.Nmax);
+    HIP_TRY(dfull.alloc(size_t(W) * L * L));
+    HIP_TRY(hipMemsetAsync(dfull.p, 0, sizeof(double) * W * L * L, pb.stream));
+    HIP_TRY(launch_bppm(ka, dseq.p, W, nullptr, dfull.p, L, nullptr, pb.stream));
+    HIP_TRY(hipMemcpyAsync(probs, dfull.p, sizeof(double) * W * L * L, hipMemcpyDeviceToHost, pb.stream));
+    HIP_TRY(hipStreamSynchronize(pb.stream));
     return ADX_OK;
 }
 

@@ -112,6 +112,8 @@ struct DevTermMap {   // per (context, term)
     int vfree, vcons;
     int favorable;
     double weight;
+    int kind;         // 0 = MacrostateProbTerm, 1 = base-pair probability term
+    int pidx;         // kind 1: index into KArgs::pairs / the per-walker pair probabilities
 };
 
 // Special-hairpin key: 3 bits per base of the closing-pair-inclusive loop.
@@ -139,6 +141,12 @@ struct KArgs {
     int n_groups2;              //   (context, macrostate); a lone variant is paired with itself)
     int opt;                    // launch-time LDS options (kernels.hip choose_opt)
     int mode;                   // 0 = partition functions, 1 = minimum free energies (MinPlus tables)
+    // base-pair probabilities (outside pass, bppm_kernel)
+    const int *bvars;           // [n_bvars] variants folded with an outside pass
+    int n_bvars;
+    const int *pairs;           // [n_pairs][3]: bvars index, i, j (1-based, folded coordinates)
+    int n_pairs;
+    const double *pair_p;       // [W][n_pairs] probabilities written by bppm_kernel (score input)
 };
 
 // Monte Carlo state (device, read/write).

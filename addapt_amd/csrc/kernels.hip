@@ -148,6 +148,7 @@ constexpr int CHUNK = 16;      // closing-pair cells per chunk of one wave (4 pr
 constexpr int GSLOTS = NG_MAX / WAVE;   // 6
 constexpr int SSLOTS = NS_MAX / WAVE;   // 2
 constexpr int LDS_LIMIT = 160 * 1024;
+constexpr int MAXLOOP_K = 30;  // largest interior loop (ViennaRNA MAXLOOP)
 
 // LDS carve-out for one workgroup folding P variants in lockstep (P = 2: the
 // apo and holo folds of one (context, macrostate), which share every cell,
@@ -1008,16 +1009,21 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 // ---------------------------------------------------------------- scoring
 // lane 0 of the block: score from the per-variant energies in L.G
 template <int P>
-__device__ double combine_score(const KArgs &ka, const Lds<P> &L, double *terms_out) {
+__device__ double combine_score(const KArgs &ka, const Lds<P> &L, const double *pp, double *terms_out) {
     const DevScaled &X = *ka.X;
     double score = 0.0;
     for (int c = 0; c < ka.n_ctx_eff; c++) {
         for (int t = 0; t < ka.n_terms; t++) {
             const DevTermMap m = ka.tmap[c * ka.n_terms + t];
-            // vrna_pf returns float (scoring.cc:58,65)
-            const double gt = static_cast<double>(static_cast<float>(L.G[m.vfree]));
-            const double ga = static_cast<double>(static_cast<float>(L.G[m.vcons]));
-            double p = exp((gt - ga) / X.kT);
+            double p;
+            if (m.kind == 1) {
+                p = pp[m.pidx];   // RnaFold::base_pair_prob (scoring.cc:37-51), bppm_kernel
+            } else {
+                // vrna_pf returns float (scoring.cc:58,65)
+                const double gt = static_cast<double>(static_cast<float>(L.G[m.vfree]));
+                const double ga = static_cast<double>(static_cast<float>(L.G[m.vcons]));
+                p = exp((gt - ga) / X.kT);
+            }
             if (!m.favorable) p = 1.0 - p;
             const double val = log(p);
             if (terms_out) terms_out[c * ka.n_terms + t] = val;
@@ -1029,7 +1035,7 @@ __device__ double combine_score(const KArgs &ka, const Lds<P> &L, double *terms_
 
 template <int NT, int P, class SR>
 __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
-                                 const uint8_t *raw, const Lds<P> &L,
+                                 const uint8_t *raw, const Lds<P> &L, const double *pp,
                                  float *dG_out, double *terms_out) {
     const int ng = P == 2 ? ka.n_groups2 : ka.n_variants;
     for (int g = 0; g < ng; g++) {
@@ -1060,7 +1066,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
             L.G[v] = g;
             if (dG_out) dG_out[v] = static_cast<float>(g);
         }
-        s = combine_score(ka, L, terms_out);
+        s = combine_score(ka, L, pp, terms_out);
     }
     return s;
 }
@@ -1079,9 +1085,305 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
-    const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, dG ? dG + size_t(w) * ka.n_variants : nullptr,
+    const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
+    const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, pp, dG ? dG + size_t(w) * ka.n_variants : nullptr,
                                           terms ? terms + size_t(w) * nt : nullptr);
     if (threadIdx.x == 0) scores[w] = s;
+}
+
+// ---------------------------------------------------------------- outside / bppm
+// Base-pair probabilities of one fold (ViennaRnaFold::base_pair_prob,
+// scoring.cc:37-51; vrna_pf with compute_bpp): P(i,j) = qb(i,j) * qbb(i,j) / Z,
+// qbb = dZ/dqb the outside (adjoint) quantity of the inside recursions of
+// pf_group, in gather form and descending span (oracle/fold.c orc_bppm is the
+// scatter form of the same sweep):
+//   q5b[m]   = [up[m+1]] sigma q5b[m+1] + sum_j q5b[j] qb(m+1,j) ext(m+1,j)
+//   qmb(i,j) = sum_{l>j} Y(i,l) qm1(j+1,l),  Y(i,l) = qmb(i,l) + X(i,l),
+//              X(i,l) = qbb(i-1,l+1) MLclosing stemM(rev(i-1,l+1))
+//   qm1b(k,l)= qmb(k,l) + sum_{i<k} [qmb(i,l) pw(k-i) + Y(i,l) qm(i,k-1)]
+//              + [up[l+1]] expMLbase sigma qm1b(k,l+1)
+//   qbb(p,q) = q5b[q] q5[p-1] ext(p,q) + qm1b(p,q) stemM(p,q)
+//              + sum_{(i,j) enclosing, loop <= 30} qbb(i,j) F_interior(i,j,p,q)
+// One wave per cell (lanes = split points / interior-loop terms), one barrier
+// per diagonal.  The interior gather mirrors qb_terms: qbb is stored times the
+// outer pair's mismatch, special loops cancel it with the same CT_* tables
+// indexed by the outer pair's code.
+struct Outs {
+    float *qbb;    // diagonal-major: qbb(i,j) * mismatchI(outer code), 0 for non-pairable cells
+    float *qmb;    // column-major colb(j)+i-1
+    float *Y;      // row-major rowb(i)+j-i-4
+    uint8_t *oc;   // diagonal-major outer code type*25 + S[i+1]*5 + S[j-1]
+    float *qm1b;   // [2][NP] the last two diagonals, by i
+    float *q5b;    // [NP]
+    float *pm;     // [NP] motif site weights qbb(o, o+L-1) * extra / Z, by site start
+};
+
+template <bool DRY>
+__host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, int Nmax, Outs *O) {
+    auto take = [&](size_t bytes) -> char * {
+        char *p = DRY ? nullptr : base + o;
+        o += (bytes + 15) & ~size_t(15);
+        return p;
+    };
+    const size_t C = size_t(cells);
+    const int NP = Nmax + 2;
+    Outs t;
+    t.qbb = reinterpret_cast<float *>(take(C * 4));
+    t.qmb = reinterpret_cast<float *>(take(C * 4));
+    t.Y = reinterpret_cast<float *>(take(C * 4));
+    t.oc = reinterpret_cast<uint8_t *>(take(C));
+    t.qm1b = reinterpret_cast<float *>(take(2 * NP * 4));
+    t.q5b = reinterpret_cast<float *>(take(NP * 4));
+    t.pm = reinterpret_cast<float *>(take(NP * 4));
+    if (!DRY) *O = t;
+    return o;
+}
+
+// full: row stride ld (folded coordinates, 0-based), pre-zeroed by the host;
+// pp: the requested pairs of this variant (KArgs::pairs with bvars index bv).
+template <int NT>
+__device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const Outs &O,
+                        const DevScaled *__restrict__ XS, float Z, double *full, int ld, double *pp) {
+    constexpr int NW = NT / WAVE;
+    const DevVariant V = ka.variants[v];
+    const int N = uni(V.N);
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int wid = uni(tid / WAVE);
+    const int NP = L.np;
+    const float *ct = L.ct;
+    const uint8_t *S = L.S;
+    const float sig1 = XS->sig[1];
+    const float mlbase_sig = XS->mlbase_sig;
+    const float mlclosing = XS->mlclosing;
+    const float eTAU = XS->ctab[CT_FSM + 6];
+    const bool motif = V.motif != 0 && XS->motif_len > 0;
+    const int mL = XS->motif_len;
+    const DevTables &T = *ka.T;
+
+    // ---- setup: outer codes, zeroed adjoints
+    for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
+        const int od = off(dd, N);
+        for (int r = lane; r < N - dd; r += WAVE) {
+            const int i = r + 1, j = i + dd;
+            O.oc[od + r] = static_cast<uint8_t>(ptype(S[i], S[j]) * 25 + S[i + 1] * 5 + S[j - 1]);
+            O.qbb[od + r] = 0.f;
+            O.qmb[colb(j) + i - 1] = 0.f;
+            O.Y[rowb(i, N) + dd - 4] = 0.f;
+        }
+    }
+    for (int k = tid; k < 2 * NP; k += NT) O.qm1b[k] = 0.f;
+    for (int k = tid; k < NP; k += NT) { O.q5b[k] = 0.f; O.pm[k] = 0.f; }
+    __syncthreads();
+
+    // ---- exterior adjoint q5b (one wave, sequential in m)
+    if (wid == 0) {
+        if (lane == 0) O.q5b[N] = 1.f;
+        float nxt = 1.f;   // q5b[m + 1]
+        for (int m = N - 1; m >= 0; m--) {
+            const int k = m + 1;
+            float acc = 0.f;
+            for (int j = k + 4 + lane; j <= N; j += WAVE) {
+                const int ix = off(j - k, N) + k - 1;
+                const int ty = ptype(S[k], S[j]);
+                const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? S[k - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
+                acc = fmaf(O.q5b[j] * L.qbm[0][ix], ct[CT_INVMM + L.cc[ix]] * e, acc);
+            }
+            const float val = ((L.up[k] >= 1) ? nxt * sig1 : 0.f) + wave_sum(acc);
+            if (lane == 0) O.q5b[m] = val;
+            nxt = val;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    __syncthreads();
+
+    // ---- per-lane term descriptors (S list: 2 slots, G list: 6 slots)
+    int sn1[SSLOTS], sn2[SSLOTS], skd[SSLOTS];
+    float sfv[SSLOTS];
+#pragma unroll
+    for (int s = 0; s < SSLOTS; s++) {
+        const int pk = int(L.sd[s * WAVE + lane]);
+        sn1[s] = pk & 255;
+        sn2[s] = (pk >> 8) & 255;
+        skd[s] = (s * WAVE + lane < XS->s_cnt[31]) ? (pk >> 16) : -1;
+        sfv[s] = L.sf[s * WAVE + lane];
+    }
+    int gn1[GSLOTS], gu[GSLOTS];
+    float gfv[GSLOTS];
+#pragma unroll
+    for (int s = 0; s < GSLOTS; s++) {
+        const int pk = L.gd[s * WAVE + lane];
+        gn1[s] = pk & 255;
+        gu[s] = (s * WAVE + lane < XS->g_cnt[31]) ? gn1[s] + (pk >> 8) : 99;
+        gfv[s] = L.gf[s * WAVE + lane];
+    }
+
+    for (int d = N - 1; d >= 4; d--) {
+        const int nc = N - d;
+        const int od = off(d, N);
+        const int umax = min(MAXLOOP_K, N - 3 - d);
+        for (int r = wid; r < nc; r += NW) {
+            const int i = r + 1, j = i + d;
+            const int idx = od + r;
+            const bool pr = !SumProd::is_mark(L.qbm[0][idx]);
+            // multiloop adjoints: split points over lanes
+            float a_qmb = 0.f, a_rest = 0.f;
+            for (int l = j + 5 + lane; l <= N; l += WAVE)
+                a_qmb = fmaf(O.Y[rowb(i, N) + l - i - 4], L.qm1[0][colb(l) + j], a_qmb);
+            for (int ip = 1 + lane; ip < i; ip += WAVE) {
+                const int t = i - ip;
+                float x = (L.up[ip] >= t) ? O.qmb[colb(j) + ip - 1] * L.pw[t] : 0.f;
+                if (t >= 5) x = fmaf(O.Y[rowb(ip, N) + j - ip - 4], L.qm[0][rowb(ip, N) + t - 5], x);
+                a_rest += x;
+            }
+            // interior loops (p, q) = (i, j) inside (a, b) = (i-1-n1, j+1+n2)
+            float a_int = 0.f;
+            if (pr) {
+                const int ccode = L.cc[idx];
+                const int ty2 = (ccode * 41) >> 10;
+                const float mmin = L.dt[DT_MMI + ccode];
+                const float tau_in = ty2 > 2 ? eTAU : 1.f;
+                const float mo_in = ct[CT_ONEN + ccode] * mmin;
+                const float m23_in = ct[CT_M23O + ccode];
+                const int A = min(int(L.dn[i - 1]), i - 2), B = min(int(L.up[j + 1]), N - 1 - j);
+                float g = 0.f;
+#pragma unroll
+                for (int s = 0; s < GSLOTS; s++) {
+                    const int n1 = gn1[s], u = gu[s], n2 = u - n1;
+                    if (u <= umax && n1 <= A && n2 <= B) {
+                        const int oidx = off(d + 2 + u, N) + i - 2 - n1;
+                        g = fmaf(O.qbb[oidx], gfv[s], g);
+                    }
+                }
+                float sp = 0.f;
+#pragma unroll
+                for (int s = 0; s < SSLOTS; s++) {
+                    const int n1 = sn1[s], n2 = sn2[s], k = skd[s], u = n1 + n2;
+                    if (k >= 0 && u <= umax && n1 <= A && n2 <= B) {
+                        const int a = i - 1 - n1, b = j + 1 + n2;
+                        const int oidx = off(d + 2 + u, N) + a - 1;
+                        const int ocd = O.oc[oidx];
+                        const int t1 = (ocd * 41) >> 10;
+                        float f;
+                        if (k == TK_STK || k == TK_B1) {
+                            f = ct[CT_INVMM + ocd] * ct[CT_STK + t1 * 8 + ty2];
+                        } else if (k == TK_BUL) {
+                            f = ct[CT_BUL + ocd] * tau_in;
+                        } else if (k == TK_1N) {
+                            f = ct[CT_ONEN + ocd] * mo_in;
+                        } else if (k == TK_M23) {
+                            f = ct[CT_INVMM + ocd] * ct[CT_M23O + ocd] * m23_in;
+                        } else {   // 1x1, 1x2, 2x1, 2x2 tables (HBM / L2)
+                            const int a1 = S[a + 1], b1 = S[b - 1], sp1 = S[i - 1], sq1 = S[j + 1];
+                            float tv;
+                            if (k == TK_I11) tv = T.int11[t1][ty2][a1][b1];
+                            else if (k == TK_I12) tv = T.int21[t1][ty2][a1][sq1][b1];
+                            else if (k == TK_I21) tv = T.int21[ty2][t1][sq1][a1][sp1];
+                            else tv = T.int22[t1][ty2][a1][sp1][sq1][b1];
+                            f = ct[CT_INVMM + ocd] * tv;
+                        }
+                        sp = fmaf(O.qbb[oidx], f * sfv[s], sp);
+                    }
+                }
+                a_int = fmaf(g, mmin, sp);
+            }
+            float s_qmb, s_rest;
+            wave_sum2<SumProd>(a_qmb, a_rest, s_qmb, s_rest);
+            const float s_int = wave_sum(a_int);
+            const float chain = (j < N && L.up[j + 1] >= 1) ? mlbase_sig * O.qm1b[((d + 1) & 1) * NP + i] : 0.f;
+            const float qm1b_v = s_qmb + s_rest + chain;
+            if (lane == 0) {
+                O.qmb[colb(j) + i - 1] = s_qmb;
+                O.Y[rowb(i, N) + d - 4] += s_qmb;     // X(i, j) was stored two diagonals ago
+                O.qm1b[(d & 1) * NP + i] = qm1b_v;
+                float qbbm = 0.f;
+                if (pr) {
+                    const int ty = ptype(S[i], S[j]);
+                    const float ext = L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
+                    const float stem = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
+                    const float qbb_v = s_int + O.q5b[j] * L.q5[0][i - 1] * ext + qm1b_v * stem;
+                    qbbm = qbb_v * L.dt[DT_MMI + O.oc[idx]];
+                    if (d - 2 >= 4)   // X(i+1, j-1): this pair closing a multiloop
+                        O.Y[rowb(i + 1, N) + d - 6] =
+                            qbb_v * mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
+                    const double qb = double(L.qbm[0][idx]) * double(ct[CT_INVMM + L.cc[idx]]);
+                    if (full) {
+                        const double pij = qb * double(qbb_v) / double(Z);
+                        full[size_t(i - 1) * ld + (j - 1)] = pij;
+                        full[size_t(j - 1) * ld + (i - 1)] = pij;
+                    }
+                    if (motif && d == mL - 1 && L.mat[i]) O.pm[i] = float(double(qbb_v) * XS->motif_extra / Z);
+                }
+                O.qbb[idx] = qbbm;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- the motif's inner pairs (the extra term at its closing cell)
+    if (motif && full && tid == 0) {
+        for (int o = 1; o + mL - 1 <= N; o++) {
+            if (O.pm[o] == 0.f) continue;
+            for (int k = 1; k < mL - 1; k++) {
+                const int pk = XS->motif_pt[k];
+                if (pk > k) {
+                    full[size_t(o + k - 1) * ld + (o + pk - 1)] += O.pm[o];
+                    full[size_t(o + pk - 1) * ld + (o + k - 1)] += O.pm[o];
+                }
+            }
+        }
+    }
+    // ---- requested pairs of this variant (score terms)
+    if (pp) {
+        for (int t = tid; t < ka.n_pairs; t += NT) {
+            if (ka.pairs[3 * t] != bv) continue;
+            const int i = ka.pairs[3 * t + 1], j = ka.pairs[3 * t + 2];
+            double pij = 0.0;
+            if (i >= 1 && j <= N && j - i >= 4) {
+                const int idx = off(j - i, N) + i - 1;
+                if (!SumProd::is_mark(L.qbm[0][idx])) {
+                    const double qb = double(L.qbm[0][idx]) * double(ct[CT_INVMM + L.cc[idx]]);
+                    const double qbb = double(O.qbb[idx]) / double(L.dt[DT_MMI + O.oc[idx]]);
+                    pij = qb * qbb / double(Z);
+                }
+                if (motif)
+                    for (int o = 1; o + mL - 1 <= N; o++) {
+                        if (O.pm[o] == 0.f || i < o || j > o + mL - 1) continue;
+                        const int pk = XS->motif_pt[i - o];
+                        if (i - o >= 1 && pk == j - o) pij += O.pm[o];
+                    }
+            }
+            pp[t] = pij;
+        }
+    }
+}
+
+// One workgroup per (walker, outside variant): inside (pf_group, P = 1) then
+// outside in LDS.  full: [W][n_bvars][ld*ld] or null; pair_p: [W][n_pairs] or null.
+template <int NT>
+__global__ void __launch_bounds__(NT, 1)
+bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
+            double *full, int ld, double *pair_p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Lds<1> L;
+    const size_t o = lds_layout<false, 1>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, false, false);
+    Outs O;
+    outs_layout<false>(smem, o, ka.cells, ka.Nmax, &O);
+    const int w = blockIdx.x / ka.n_bvars, bv = blockIdx.x % ka.n_bvars;
+    if (w >= W) return;
+    if (mask && mask[w] != 1) return;
+    load_ctab(ka, L);
+    for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
+    __syncthreads();
+    const int v = ka.bvars[bv];
+    const int vs[1] = {v};
+    float z[1];
+    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z);
+    __syncthreads();
+    outside<NT>(ka, v, bv, L, O, XS, z[0],
+                full ? full + (size_t(w) * ka.n_bvars + bv) * size_t(ld) * ld : nullptr, ld,
+                pair_p ? pair_p + size_t(w) * ka.n_pairs : nullptr);
 }
 
 // ---------------------------------------------------------------- mt19937
@@ -1371,12 +1673,40 @@ hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, doubl
     return launch_score_m(ka, seqs, W, scores, terms, dG, nullptr, stream);
 }
 
+// outside pass: LDS bytes (0 when it does not fit one CU) and launch
+size_t bppm_lds_bytes(const KArgs &ka) {
+    const size_t o = lds_layout<true, 1>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, false, false);
+    const size_t t = outs_layout<true>(nullptr, o, ka.cells, ka.Nmax, nullptr);
+    return t <= size_t(LDS_LIMIT) ? t : 0;
+}
+
+hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
+                       double *pair_p, hipStream_t stream) {
+    const size_t lds = bppm_lds_bytes(ka);
+    if (lds == 0 || ka.n_bvars <= 0) return hipErrorInvalidValue;
+    auto k = bppm_kernel<512>;
+    static size_t configured = 0;
+    if (lds > configured) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        configured = lds;
+    }
+    hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p);
+    return hipGetLastError();
+}
+
 // evs (optional): 2 * nsteps events recorded around each step's score launch
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
     for (int s = 0; s < st.nsteps; s++) {
         hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
+        if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
+            hipError_t e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0,
+                                       const_cast<double *>(ka.pair_p), stream);
+            if (e != hipSuccess) return e;
+        }
         if (evs) (void)hipEventRecord(evs[2 * s], stream);
         hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);

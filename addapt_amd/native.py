@@ -19,6 +19,7 @@ APO, HOLO = 0, 1
 THERMO_FIXED, THERMO_ANNEAL, THERMO_AUTO = 0, 1, 2
 MOTIF_ADD, MOTIF_REPLACE = 0, 1
 FOLD_PF, FOLD_MFE = 0, 1
+TERM_MACROSTATE, TERM_PAIR = 0, 1
 OUTCOMES = ["REJECT", "ACCEPT_WORSENED", "ACCEPT_UNCHANGED", "ACCEPT_IMPROVED"]
 
 
@@ -30,7 +31,7 @@ class AdxError(RuntimeError):
 
 class Term(C.Structure):
     _fields_ = [("condition", C.c_int), ("macrostate", C.c_int), ("favorable", C.c_int),
-                ("weight", C.c_double)]
+                ("weight", C.c_double), ("kind", C.c_int), ("pair_i", C.c_int), ("pair_j", C.c_int)]
 
 
 class Thermostat(C.Structure):
@@ -72,7 +73,7 @@ EXPORTS = [
     "adx_fold_pf", "adx_fold_mfe", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
     "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
-    "adx_walkers_import", "adx_set_temperature",
+    "adx_walkers_import", "adx_set_temperature", "adx_bppm_batch",
 ]
 
 _lib = None
@@ -112,6 +113,8 @@ def lib():
                                            C.POINTER(C.c_int64)]
         L.adx_score_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double), C.POINTER(C.c_float)]
+        L.adx_bppm_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.c_int,
+                                     C.POINTER(C.c_double)]
         L.adx_variant_desc.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int),
                                        C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _lib = L
@@ -210,7 +213,9 @@ def make_thermostat(kind="fixed", t=1.0, t_hi=1.0, t_lo=0.0, cycle_len=1, rate=0
 class Engine:
     """Batched Monte Carlo context (adx_ctx_*).
 
-    terms: list of (condition 'apo'|'holo', macrostate index, favorable bool, weight)
+    terms: list of (condition 'apo'|'holo', target, favorable bool, weight); target is a
+    macrostate index (MacrostateProbTerm) or ("pair", i, j) (base-pair probability term,
+    0-based device positions)
     aptamer: None or (seq, fold, energy_kcal); contexts: list of (before, after).
     fold_mode: "pf" (ensembles, vrna_pf) or "mfe" (minimum free energies, ADX_FOLD_MFE).
     """
@@ -227,7 +232,11 @@ class Engine:
         d.macrostates = self._ms
         self._terms = (Term * max(1, len(terms)))()
         for k, (cond, mi, fav, w) in enumerate(terms):
-            self._terms[k] = Term(HOLO if cond in ("holo", HOLO) else APO, mi, int(bool(fav)), w)
+            c = HOLO if cond in ("holo", HOLO) else APO
+            if isinstance(mi, tuple):
+                self._terms[k] = Term(c, 0, int(bool(fav)), w, TERM_PAIR, mi[1], mi[2])
+            else:
+                self._terms[k] = Term(c, mi, int(bool(fav)), w, TERM_MACROSTATE, 0, 0)
         d.n_terms = len(terms)
         d.terms = self._terms
         if aptamer is not None:
@@ -239,6 +248,7 @@ class Engine:
             self._ctx[k] = ContextDesc(_b(b), _b(a))
         d.n_contexts = len(ctx)
         d.contexts = self._ctx
+        self._ctx_lens = [(len(b), len(a)) for b, a in ctx]
         d.thermostat = thermostat if thermostat is not None else make_thermostat()
         d.device = device
         d.fold_mode = {"pf": FOLD_PF, "mfe": FOLD_MFE}[fold_mode]
@@ -271,6 +281,19 @@ class Engine:
                                      tv.ctypes.data_as(C.POINTER(C.c_double)),
                                      dg.ctypes.data_as(C.POINTER(C.c_float))))
         return sc, tv.reshape(W, -1)[:, :self.n_terms_total], dg.reshape(W, -1)
+
+    def bppm_batch(self, seqs, condition="apo", context=0):
+        """(W, L, L) base-pair probability matrices of the (context, condition) fold."""
+        W = len(seqs)
+        buf = b"".join(_b(s) for s in seqs)
+        c = HOLO if condition in ("holo", HOLO) else APO
+        L = self.N
+        if self._ctx_lens:
+            L += sum(self._ctx_lens[context])
+        out = np.zeros(W * L * L, np.float64)
+        _check(lib().adx_bppm_batch(self.ptr, W, buf, c, context,
+                                    out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out.reshape(W, L, L)
 
     def walkers_init(self, seeds, seqs=None):
         W = len(seeds)

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ADX_ABI_VERSION 2
+#define ADX_ABI_VERSION 3
 
 typedef enum adx_status {
     ADX_OK = 0,
@@ -93,11 +93,17 @@ void adx_fold_free(adx_fold *f);
 #define ADX_APO 0
 #define ADX_HOLO 1
 
-typedef struct adx_term {      /* MacrostateProbTerm (scoring.hh:175-192) */
+#define ADX_TERM_MACROSTATE 0  /* MacrostateProbTerm (scoring.hh:175-192): p = macrostate_prob */
+#define ADX_TERM_PAIR 1        /* p = RnaFold::base_pair_prob(i, j) (scoring.cc:37-51) of the
+                                  condition's unconstrained fold (outside pass, configs 3-4) */
+
+typedef struct adx_term {
     int condition;             /* ADX_APO / ADX_HOLO */
-    int macrostate;            /* index into adx_run_desc.macrostates */
-    int favorable;             /* 1 = "<name>", 0 = "not <name>" */
+    int macrostate;            /* index into adx_run_desc.macrostates (ADX_TERM_MACROSTATE) */
+    int favorable;             /* 1 = "<name>" (ln p), 0 = "not <name>" (ln(1 - p)) */
     double weight;             /* ScoreTerm weight (scoring.hh:160-168) */
+    int kind;                  /* ADX_TERM_MACROSTATE (zero-initialised default) / ADX_TERM_PAIR */
+    int pair_i, pair_j;        /* ADX_TERM_PAIR: 0-based device positions, i < j */
 } adx_term;
 
 #define ADX_THERMO_FIXED 0     /* FixedThermostat (sampling.cc:305-321) */
@@ -208,6 +214,14 @@ adx_status adx_set_temperature(adx_ctx *ctx, double t);
  * dG[W*n_variants] ensemble energies (kcal/mol, float, optional). */
 adx_status adx_score_batch(adx_ctx *ctx, int n_walkers, const char *seqs, double *scores,
                            double *term_values, float *dG);
+
+/* Base-pair probability matrices of W sequences (W*N chars) for one
+ * (context, condition) unconstrained fold: probs = W * L * L doubles, L the
+ * folded (context-padded) length, row-major, symmetric, zero diagonal --
+ * probs[w*L*L + (i-1)*L + (j-1)] = fc->exp_matrices->probs[iindx[i]-j]
+ * (scoring.cc:47-50).  context = 0 without contexts. */
+adx_status adx_bppm_batch(adx_ctx *ctx, int n_walkers, const char *seqs, int condition, int context,
+                          double *probs);
 
 /* Variant v of the score: which (context, condition, macrostate or -1). */
 adx_status adx_variant_desc(const adx_ctx *ctx, int v, int *context, int *condition,

@@ -141,9 +141,13 @@ int orc_mutate_recursively(char *seq, int n, const char *const *macrostates, int
 /* ---- score function + Monte Carlo ------------------------------------- */
 typedef struct orc_term {
     int condition;  /* 0 = apo, 1 = holo */
-    int macrostate; /* index into the macrostate list */
+    int macrostate; /* index into the macrostate list (kind 0) */
     int favorable;  /* 1 = YES, 0 = NO ("not <name>") */
     double weight;
+    int kind;       /* 0 = MacrostateProbTerm (scoring.cc:233-259); 1 = base-pair
+                       probability term: p = RnaFold::base_pair_prob(i, j) of the
+                       condition's unconstrained fold (scoring.cc:37-51) */
+    int pair_i, pair_j; /* kind 1: 0-based device positions (context-shifted) */
 } orc_term;
 
 typedef struct orc_context {

@@ -139,13 +139,24 @@ static double macrostate_prob(const orc_params *P, const char *seq, const char *
 }
 
 static double evaluate_terms(const orc_scorefxn *sf, const char *seq, const char *const *ms,
-                             double *tv) {
+                             int off, double *tv) {
     double score = 0.0;
+    const int L = (int)strlen(seq);
+    double *bpp[2] = {NULL, NULL};   /* per condition, computed on first use (scoring.cc:41-44) */
     for (int t = 0; t < sf->n_terms; t++) {
         const orc_term *T = &sf->terms[t];
         const orc_motif *motif = (T->condition == 1) ? sf->aptamer : NULL;
         double p;
-        if (sf->mode == 1) {
+        if (T->kind == 1) {
+            /* ViennaRnaFold::base_pair_prob (scoring.cc:37-51): unconstrained ensemble */
+            double **B = &bpp[T->condition == 1];
+            if (!*B) {
+                *B = (double *)malloc(sizeof(double) * (size_t)L * L);
+                orc_bppm(sf->P, seq, NULL, motif, *B);
+            }
+            int a = T->pair_i + off, b = T->pair_j + off;
+            p = (a != b && a >= 0 && b >= 0 && a < L && b < L) ? (*B)[(size_t)a * L + b] : 0.0;
+        } else if (sf->mode == 1) {
             /* MFE image of macrostate_prob: float-rounded like vrna_mfe's return */
             double gt = (float)orc_mfe_energy(sf->P, seq, NULL, motif);
             double ga = (float)orc_mfe_energy(sf->P, seq, ms[T->macrostate], motif);
@@ -158,6 +169,8 @@ static double evaluate_terms(const orc_scorefxn *sf, const char *seq, const char
         if (tv) tv[t] = v;
         score += T->weight * v;
     }
+    free(bpp[0]);
+    free(bpp[1]);
     return score;
 }
 
@@ -167,7 +180,7 @@ double orc_score(const orc_scorefxn *sf, const char *seq, int n, const char *con
         char *s = (char *)malloc(n + 1);
         memcpy(s, seq, n);
         s[n] = 0;
-        double r = evaluate_terms(sf, s, ms, tv);
+        double r = evaluate_terms(sf, s, ms, 0, tv);
         free(s);
         return r;
     }
@@ -187,7 +200,7 @@ double orc_score(const orc_scorefxn *sf, const char *seq, int n, const char *con
             memcpy(pm[m] + lb, ms[m], n);
             pm[m][L] = 0;
         }
-        score += evaluate_terms(sf, s, (const char *const *)pm, tv ? tv + c * sf->n_terms : NULL);
+        score += evaluate_terms(sf, s, (const char *const *)pm, lb, tv ? tv + c * sf->n_terms : NULL);
         for (int m = 0; m < nm; m++) free(pm[m]);
         free(pm);
         free(s);

@@ -31,7 +31,7 @@ class Motif(C.Structure):
 
 class Term(C.Structure):
     _fields_ = [("condition", C.c_int), ("macrostate", C.c_int), ("favorable", C.c_int),
-                ("weight", C.c_double)]
+                ("weight", C.c_double), ("kind", C.c_int), ("pair_i", C.c_int), ("pair_j", C.c_int)]
 
 
 class Context(C.Structure):
@@ -239,13 +239,18 @@ def can_be_freely_mutated(seq, macrostates, pos):
 
 
 class ScoreFunction:
-    """terms: list of (condition 'apo'/'holo', macrostate index, favorable bool, weight)."""
+    """terms: list of (condition 'apo'/'holo', target, favorable bool, weight) where
+    target is a macrostate index (MacrostateProbTerm) or ("pair", i, j) (base-pair
+    probability term, 0-based device positions)."""
 
     def __init__(self, terms, aptamer=None, contexts=None, params=None, mode="pf"):
         self.P = params or default_params()
         self._terms = (Term * max(1, len(terms)))()
         for k, (cond, mi, fav, w) in enumerate(terms):
-            self._terms[k] = Term(1 if cond == "holo" else 0, mi, 1 if fav else 0, w)
+            if isinstance(mi, tuple):
+                self._terms[k] = Term(1 if cond == "holo" else 0, 0, 1 if fav else 0, w, 1, mi[1], mi[2])
+            else:
+                self._terms[k] = Term(1 if cond == "holo" else 0, mi, 1 if fav else 0, w, 0, 0, 0)
         self._apt = aptamer
         ctx = contexts or []
         self._ctx = (Context * max(1, len(ctx)))()

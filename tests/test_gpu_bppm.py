@@ -1,0 +1,144 @@
+"""GPU parity of the outside pass / base-pair probabilities (SURVEY.md §8 A16,
+configs 3-4): RnaFold::base_pair_prob (scoring.cc:37-51) through adx_fold_bpp,
+adx_bppm_batch and the ADX_TERM_PAIR score term, against the oracle's FP64
+adjoint sweep (oracle/fold.c orc_bppm).
+
+Tolerances: FP32 inside + outside with per-nucleotide scaling vs FP64:
+|P_gpu - P_oracle| <= 2e-4 absolute per pair; ln p terms within 2e-3 where
+p (or 1 - p) >= 1e-2; MC trajectories bit-exact with the oracle forced through
+Metropolis near-ties (|crit - u| <= 2e-3).
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from addapt_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+P_TOL = 2e-4
+
+
+def rand_seq(rng, n):
+    return "".join(rng.choice("ACGU") for _ in range(n))
+
+
+def test_fold_bpp_matches_oracle(native, oracle):
+    rng = random.Random(23)
+    cases = [("GGGGAAACCCC", None), ("ACGUGAAAACGU", "((((....))))"), (workloads.THEO_SEQ, None)]
+    for n in (20, 45, 80, 100):
+        for _ in range(2):
+            cases.append((rand_seq(rng, n), None))
+    cases.append((cases[-1][0], "." * 10 + "x" * 5 + "." * 85))
+    for seq, cst in cases:
+        f = native.Fold(seq)
+        if cst:
+            f.add_constraint(cst)
+        _, ref = oracle.bppm(seq, cst)
+        n = len(seq)
+        got = np.array([[f.bpp(i + 1, j + 1) for j in range(n)] for i in range(n)])
+        assert np.abs(got - ref).max() <= P_TOL, (seq, cst, np.abs(got - ref).max())
+
+
+def test_fold_bpp_motif(native, oracle):
+    apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
+    e = oracle.theo_bonus()
+    for seq in (apt, "GGGA" + apt + "UCCC"):
+        f = native.Fold(seq)
+        f.add_motif(apt, fold, e)
+        _, ref = oracle.bppm(seq, None, oracle.make_motif(apt, fold, e, 0))
+        n = len(seq)
+        got = np.array([[f.bpp(i + 1, j + 1) for j in range(n)] for i in range(n)])
+        assert np.abs(got - ref).max() <= P_TOL, (seq, np.abs(got - ref).max())
+
+
+def _objective(N):
+    # config 3: default objective + apo/holo base-pair probability terms
+    return workloads.default_objective() + [("apo", ("pair", 0, N - 1), False, 1.0),
+                                            ("holo", ("pair", 0, N - 1), True, 1.0)]
+
+
+def _engine(native, tmpl, macro, terms, thermostat=None, contexts=None):
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    return native.Engine(tmpl, macro, terms, aptamer=apt, contexts=contexts,
+                         thermostat=thermostat or native.make_thermostat("fixed", t=1.0))
+
+
+def _oracle_sf(oracle, terms, contexts=None):
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts)
+
+
+@pytest.mark.parametrize("N", [60, 100])
+def test_bppm_batch(native, oracle, N):
+    tmpl, active = workloads.synthetic(N)
+    eng = _engine(native, tmpl, [active], _objective(N))
+    seqs = workloads.walker_sequences(tmpl, [active], 6)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    for cond in ("apo", "holo"):
+        got = eng.bppm_batch(seqs, cond)
+        for w in range(6):
+            _, ref = oracle.bppm(seqs[w].upper(), None, m if cond == "holo" else None)
+            err = np.abs(got[w] - ref).max()
+            assert err <= P_TOL, (N, cond, w, err)
+
+
+def _close_term(a, b):
+    if math.isinf(b):
+        return a == b
+    return abs(a - b) <= 2e-3 or abs(math.exp(a) - math.exp(b)) <= P_TOL
+
+
+@pytest.mark.parametrize("N", [60, 100])
+def test_score_with_pair_terms(native, oracle, N):
+    tmpl, active = workloads.synthetic(N)
+    terms = _objective(N)
+    eng = _engine(native, tmpl, [active], terms)
+    seqs = workloads.walker_sequences(tmpl, [active], 12)
+    sc, tv, _ = eng.score_batch(seqs)
+    sf = _oracle_sf(oracle, terms)
+    for w in range(12):
+        ref, tref = sf.score(seqs[w], [active])
+        for a, b in zip(tv[w], tref):
+            assert _close_term(a, b), (w, list(tv[w]), tref)
+
+
+def test_pair_terms_with_contexts(native, oracle):
+    tmpl, active = workloads.synthetic(60)
+    terms = [("apo", ("pair", 2, 57), True, 1.0), ("holo", ("pair", 0, 59), False, 0.5),
+             ("holo", 0, True, 1.0)]
+    ctx = [("GGAC", "UUA"), ("", "CCCA")]
+    eng = _engine(native, tmpl, [active], terms, contexts=ctx)
+    seqs = workloads.walker_sequences(tmpl, [active], 4)
+    sc, tv, _ = eng.score_batch(seqs)
+    sf = _oracle_sf(oracle, terms, contexts=ctx)
+    for w in range(4):
+        ref, tref = sf.score(seqs[w], [active])
+        for a, b in zip(tv[w], tref):
+            assert _close_term(a, b), (w, list(tv[w]), tref)
+
+
+def test_mc_trajectory_with_pair_terms(native, oracle):
+    tmpl, active = workloads.synthetic(60)
+    terms = _objective(60)
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [0, 1, 2, 3]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    steps = 25
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=2e-3)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert tr["base"][w::len(seeds)] == ref["base"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert list(counters[w]) == ref["counters"]
