@@ -25,9 +25,10 @@ size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
 hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
                         double *terms, float *dG, hipStream_t stream);
 hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream, hipEvent_t *evs);
-size_t bppm_lds_bytes(const KArgs &ka);
+size_t bppm_lds_bytes(const KArgs &ka, bool *gout);
+size_t bppm_scratch_bytes(const KArgs &ka, int W);
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
-                       double *pair_p, hipStream_t stream);
+                       double *pair_p, char *scratch, hipStream_t stream);
 constexpr int NT = 512;
 constexpr size_t LDS_MAX = 163840;
 }  // namespace adx
@@ -416,6 +417,7 @@ struct Problem {
     std::vector<int> pairs;      // [n][3]: bvars index, i, j (1-based folded coordinates)
     DevBuf<int> dBvars, dPairs;
     DevBuf<double> dPairP;
+    DevBuf<char> dScratch;       // outside tables in HBM when they do not fit LDS
     std::unique_ptr<DevTables> hT;
     std::unique_ptr<DevScaled> hX;
 
@@ -463,6 +465,7 @@ struct Problem {
         ka.pairs = dPairs.p;
         ka.n_pairs = static_cast<int>(pairs.size() / 3);
         ka.pair_p = dPairP.p;
+        ka.bppm_scratch = dScratch.p;
         return ka;
     }
 
@@ -521,7 +524,7 @@ struct Problem {
         HIP_TRY(dBvars.upload(bvars.data(), bvars.size(), stream));
         HIP_TRY(dPairs.upload(pairs.data(), pairs.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
-        if (!pairs.empty() && bppm_lds_bytes(kargs()) == 0)
+        if (!pairs.empty() && bppm_lds_bytes(kargs(), nullptr) == 0)
             return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", Nmax);
         return choose_layout();
     }
@@ -530,6 +533,11 @@ struct Problem {
     adx_status ensure_pairs(int W) {
         const size_t need = size_t(W) * (pairs.size() / 3);
         if (need > 0 && dPairP.n < need) HIP_TRY(dPairP.alloc(need));
+        return ensure_scratch(kargs(), W);
+    }
+    adx_status ensure_scratch(const KArgs &ka, int W) {
+        const size_t need = bppm_scratch_bytes(ka, W);
+        if (need > 0 && dScratch.n < need) HIP_TRY(dScratch.alloc(need));
         return ADX_OK;
     }
 
@@ -538,7 +546,7 @@ struct Problem {
         if (!pairs.empty()) {
             adx_status s = ensure_pairs(W);
             if (s) return s;
-            HIP_TRY(launch_bppm(kargs(), dseqs, W, nullptr, nullptr, 0, dPairP.p, stream));
+            HIP_TRY(launch_bppm(kargs(), dseqs, W, nullptr, nullptr, 0, dPairP.p, dScratch.p, stream));
         }
         HIP_TRY(launch_score(kargs(), qbm, dseqs, W, dscores, dterms, ddG, stream));
         return ADX_OK;
@@ -694,13 +702,15 @@ static adx_status fold_energy(adx_fold *f, int mode, float *energy, std::vector<
         if (!std::isfinite(g)) return ADX_OK;   // empty ensemble: every probability is 0
         pb.bvars.assign(1, 0);
         HIP_TRY(pb.dBvars.upload(pb.bvars.data(), 1, pb.stream));
-        const KArgs ka = pb.kargs();
-        if (bppm_lds_bytes(ka) == 0)
+        if (bppm_lds_bytes(pb.kargs(), nullptr) == 0)
             return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", N);
+        s = pb.ensure_scratch(pb.kargs(), 1);
+        if (s) return s;
+        const KArgs ka = pb.kargs();
         DevBuf<double> dfull;
         HIP_TRY(dfull.alloc(size_t(N) * N));
         HIP_TRY(hipMemsetAsync(dfull.p, 0, sizeof(double) * N * N, pb.stream));
-        HIP_TRY(launch_bppm(ka, dseq.p, 1, nullptr, dfull.p, N, nullptr, pb.stream));
+        HIP_TRY(launch_bppm(ka, dseq.p, 1, nullptr, dfull.p, N, nullptr, ka.bppm_scratch, pb.stream));
         HIP_TRY(hipMemcpyAsync(bpp->data(), dfull.p, sizeof(double) * N * N, hipMemcpyDeviceToHost, pb.stream));
         HIP_TRY(hipStreamSynchronize(pb.stream));
     }
@@ -1266,11 +1276,15 @@ extern "C" adx_status adx_bppm_batch(adx_ctx *c, int W, const char *seqs, int co
     ka.n_pairs = 0;
     ka.pairs = nullptr;
     ka.pair_p = nullptr;
-    if (bppm_lds_bytes(ka) == 0)
+    if (bppm_lds_bytes(ka, nullptr) == 0)
         return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", pb.Nmax);
+    DevBuf<char> dscr;
+    const size_t scr = bppm_scratch_bytes(ka, W);
+    if (scr) HIP_TRY(dscr.alloc(scr));
+    ka.bppm_scratch = dscr.p;
     HIP_TRY(dfull.alloc(size_t(W) * L * L));
     HIP_TRY(hipMemsetAsync(dfull.p, 0, sizeof(double) * W * L * L, pb.stream));
-    HIP_TRY(launch_bppm(ka, dseq.p, W, nullptr, dfull.p, L, nullptr, pb.stream));
+    HIP_TRY(launch_bppm(ka, dseq.p, W, nullptr, dfull.p, L, nullptr, ka.bppm_scratch, pb.stream));
     HIP_TRY(hipMemcpyAsync(probs, dfull.p, sizeof(double) * W * L * L, hipMemcpyDeviceToHost, pb.stream));
     HIP_TRY(hipStreamSynchronize(pb.stream));
     return ADX_OK;

@@ -147,6 +147,7 @@ struct KArgs {
     const int *pairs;           // [n_pairs][3]: bvars index, i, j (1-based, folded coordinates)
     int n_pairs;
     const double *pair_p;       // [W][n_pairs] probabilities written by bppm_kernel (score input)
+    char *bppm_scratch;         // global outside tables when they do not fit LDS (N >~ 110)
 };
 
 // Monte Carlo state (device, read/write).

@@ -1118,25 +1118,40 @@ struct Outs {
     float *pm;     // [NP] motif site weights qbb(o, o+L-1) * extra / Z, by site start
 };
 
-template <bool DRY>
-__host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, int Nmax, Outs *O) {
+// LDS carve of the outside arrays after the inside layout.  GOUT: the four
+// cell tables live in a per-workgroup global scratch slice instead (devices
+// whose inside + outside tables exceed one CU's LDS, e.g. N = 150); the rest
+// stays in LDS.
+template <bool DRY, bool GOUT>
+__host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, int Nmax, Outs *O,
+                                              char *gbase = nullptr) {
     auto take = [&](size_t bytes) -> char * {
         char *p = DRY ? nullptr : base + o;
         o += (bytes + 15) & ~size_t(15);
         return p;
     };
+    size_t g = 0;
+    auto gtake = [&](size_t bytes) -> char * {
+        char *p = DRY ? nullptr : gbase + g;
+        g += (bytes + 15) & ~size_t(15);
+        return p;
+    };
     const size_t C = size_t(cells);
     const int NP = Nmax + 2;
     Outs t;
-    t.qbb = reinterpret_cast<float *>(take(C * 4));
-    t.qmb = reinterpret_cast<float *>(take(C * 4));
-    t.Y = reinterpret_cast<float *>(take(C * 4));
-    t.oc = reinterpret_cast<uint8_t *>(take(C));
+    t.qbb = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
+    t.qmb = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
+    t.Y = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
+    t.oc = reinterpret_cast<uint8_t *>(GOUT ? gtake(C) : take(C));
     t.qm1b = reinterpret_cast<float *>(take(2 * NP * 4));
     t.q5b = reinterpret_cast<float *>(take(NP * 4));
     t.pm = reinterpret_cast<float *>(take(NP * 4));
     if (!DRY) *O = t;
     return o;
+}
+// global scratch bytes per workgroup of the GOUT layout
+__host__ __device__ inline size_t outs_global_bytes(int cells) {
+    return 3 * ((size_t(cells) * 4 + 15) & ~size_t(15)) + ((size_t(cells) + 15) & ~size_t(15));
 }
 
 // full: row stride ld (folded coordinates, 0-based), pre-zeroed by the host;
@@ -1360,16 +1375,18 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
 }
 
 // One workgroup per (walker, outside variant): inside (pf_group, P = 1) then
-// outside in LDS.  full: [W][n_bvars][ld*ld] or null; pair_p: [W][n_pairs] or null.
-template <int NT>
+// outside.  full: [W][n_bvars][ld*ld] or null; pair_p: [W][n_pairs] or null;
+// GOUT: gscratch holds gridDim.x slices of outs_global_bytes.
+template <int NT, bool GOUT>
 __global__ void __launch_bounds__(NT, 1)
 bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
-            double *full, int ld, double *pair_p) {
+            double *full, int ld, double *pair_p, char *gscratch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<1> L;
     const size_t o = lds_layout<false, 1>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, false, false);
     Outs O;
-    outs_layout<false>(smem, o, ka.cells, ka.Nmax, &O);
+    outs_layout<false, GOUT>(smem, o, ka.cells, ka.Nmax, &O,
+                             GOUT ? gscratch + size_t(blockIdx.x) * outs_global_bytes(ka.cells) : nullptr);
     const int w = blockIdx.x / ka.n_bvars, bv = blockIdx.x % ka.n_bvars;
     if (w >= W) return;
     if (mask && mask[w] != 1) return;
@@ -1673,18 +1690,29 @@ hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, doubl
     return launch_score_m(ka, seqs, W, scores, terms, dG, nullptr, stream);
 }
 
-// outside pass: LDS bytes (0 when it does not fit one CU) and launch
-size_t bppm_lds_bytes(const KArgs &ka) {
+// outside pass: LDS bytes of the all-LDS layout, or of the global-scratch
+// layout (gout = true) when that does not fit; 0 when neither fits one CU.
+size_t bppm_lds_bytes(const KArgs &ka, bool *gout) {
     const size_t o = lds_layout<true, 1>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, false, false);
-    const size_t t = outs_layout<true>(nullptr, o, ka.cells, ka.Nmax, nullptr);
-    return t <= size_t(LDS_LIMIT) ? t : 0;
+    const size_t t = outs_layout<true, false>(nullptr, o, ka.cells, ka.Nmax, nullptr);
+    if (t <= size_t(LDS_LIMIT)) {
+        if (gout) *gout = false;
+        return t;
+    }
+    const size_t tg = outs_layout<true, true>(nullptr, o, ka.cells, ka.Nmax, nullptr);
+    if (gout) *gout = true;
+    return tg <= size_t(LDS_LIMIT) ? tg : 0;
+}
+size_t bppm_scratch_bytes(const KArgs &ka, int W) {
+    bool gout = false;
+    if (bppm_lds_bytes(ka, &gout) == 0 || !gout) return 0;
+    return size_t(W) * ka.n_bvars * outs_global_bytes(ka.cells);
 }
 
-hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
-                       double *pair_p, hipStream_t stream) {
-    const size_t lds = bppm_lds_bytes(ka);
-    if (lds == 0 || ka.n_bvars <= 0) return hipErrorInvalidValue;
-    auto k = bppm_kernel<512>;
+template <bool GOUT>
+static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs, int W, const int *mask,
+                                double *full, int ld, double *pair_p, char *scratch, hipStream_t stream) {
+    auto k = bppm_kernel<512, GOUT>;
     static size_t configured = 0;
     if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
@@ -1692,8 +1720,19 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
         if (e != hipSuccess) return e;
         configured = lds;
     }
-    hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p);
+    hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p,
+                       scratch);
     return hipGetLastError();
+}
+
+// scratch: bppm_scratch_bytes(ka, W) bytes of device memory (null when 0)
+hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
+                       double *pair_p, char *scratch, hipStream_t stream) {
+    bool gout = false;
+    const size_t lds = bppm_lds_bytes(ka, &gout);
+    if (lds == 0 || ka.n_bvars <= 0 || (gout && !scratch)) return hipErrorInvalidValue;
+    if (gout) return launch_bppm_t<true>(ka, lds, seqs, W, mask, full, ld, pair_p, scratch, stream);
+    return launch_bppm_t<false>(ka, lds, seqs, W, mask, full, ld, pair_p, nullptr, stream);
 }
 
 // evs (optional): 2 * nsteps events recorded around each step's score launch
@@ -1704,7 +1743,7 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
         if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
             hipError_t e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0,
-                                       const_cast<double *>(ka.pair_p), stream);
+                                       const_cast<double *>(ka.pair_p), ka.bppm_scratch, stream);
             if (e != hipSuccess) return e;
         }
         if (evs) (void)hipEventRecord(evs[2 * s], stream);

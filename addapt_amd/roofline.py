@@ -13,6 +13,10 @@ oracle (the product may not call the checker).
 
 The MFE (min-plus) pass visits the same terms: 2 ops per interior term
 (c[p][q] + E, min) and 2 per multiloop / split term (add, min).
+
+The outside pass (bppm_kernel) gathers the same interior terms (3 FLOP each)
+and two multiloop sums per cell: qmb (N - j - 4 split terms, 2 FLOP) and qm1b
+(i - 1 terms of two products, 4 FLOP).
 """
 import numpy as np
 
@@ -103,3 +107,14 @@ def pf_flops(seq, cst=None):
 def mfe_ops(seq, cst=None):
     a, b = pf_terms(seq, cst)
     return 2 * a + 2 * b
+
+
+def outside_flops(seq, cst=None):
+    a, _ = pf_terms(seq, cst)
+    N = len(seq)
+    ml = 0
+    for d in range(4, N):
+        for i in range(1, N - d + 1):
+            j = i + d
+            ml += 2 * max(0, N - j - 4) + 4 * (i - 1)
+    return 3 * a + ml

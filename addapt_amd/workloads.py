@@ -117,6 +117,16 @@ def walker_sequences(template, macrostates, W, seed_base=1000):
     return out
 
 
+def config_objective(N, bppm=False, active_index=0):
+    """Objective of the bench configs: the default objective (configs 2, 5), plus
+    (configs 3-4) apo/holo base-pair probability terms on the outermost pair of
+    the enforced helix: apo "not pair(0, N-1)", holo "pair(0, N-1)"."""
+    terms = default_objective(active_index)
+    if bppm:
+        terms = terms + [("apo", ("pair", 0, N - 1), False, 1.0), ("holo", ("pair", 0, N - 1), True, 1.0)]
+    return terms
+
+
 def default_objective(active_index=0):
     """objective: {apo: "not active", holo: "active"} (config.cc:72-81)."""
     return [("apo", active_index, False, 1.0), ("holo", active_index, True, 1.0)]

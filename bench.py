@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--length", type=int, default=100)
     ap.add_argument("--fold", choices=("mfe", "pf"), default="mfe",
                     help="mfe = BASELINE configs[1] (default); pf = partition-function objective")
+    ap.add_argument("--bppm", action="store_true",
+                    help="configs 3/4: add apo/holo base-pair probability terms (outside pass; --fold pf)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="approximate budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -55,14 +57,14 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold):
+def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
     """Oracle MC (the C++-equivalent CPU restatement, 'port') on the host cores."""
     from oracle import oracle as O
     from addapt_amd import workloads
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
-    sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif, mode=fold)
+    sf = O.ScoreFunction(terms, aptamer=motif, mode=fold)
     th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     # probe: 1 walker x 4 steps on one thread to size the sample
     t_probe, _ = O.mc_run_batch(sf, walker_seqs[:1], [active], th, [0], 4, 1)
@@ -99,8 +101,10 @@ def main():
 
     from addapt_amd import native, roofline, shard, workloads
 
+    if a.bppm:
+        a.fold = "pf"
     tmpl, active = workloads.synthetic(a.length)
-    terms = workloads.default_objective()
+    terms = workloads.config_objective(a.length, bppm=a.bppm)
     apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
     replica_mode = a.replica_interval > 0 and world > 1
     if replica_mode:
@@ -152,6 +156,9 @@ def main():
     f_free = sum(work(s, None) for s in sample) / len(sample)
     f_act = sum(work(s, active) for s in sample) / len(sample)
     flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
+    if a.bppm:   # bppm_kernel: inside + outside of the apo and holo unconstrained folds
+        f_out = sum(roofline.outside_flops(s, None) for s in sample) / len(sample)
+        flop_per_scored += 2 * (f_free + f_out)
     launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
     achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
     traffic, traffic_src = None, None
@@ -201,13 +208,17 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
-                        "0.32 uM), 4 %s per scored step, synthetic %d-nt sgRNA template "
+                        "0.32 uM)%s, 4 %s%s per scored step, synthetic %d-nt sgRNA template "
                         "(SURVEY.md 8d), %d walkers per GPU, annealing 5 to 0 in 300 steps"
                         % ("BASELINE configs[1] (MFE-fold score only)" if a.fold == "mfe"
-                           else "partition-function score (config 3 without bppm)",
+                           else ("BASELINE config 3/4 (pf + bppm score)" if a.bppm
+                                 else "partition-function score (config 3 without bppm)"),
+                           " + apo 'not pair(0,N-1)' / holo 'pair(0,N-1)'" if a.bppm else "",
                            "minimum-free-energy folds" if a.fold == "mfe" else "McCaskill inside PFs",
+                           " + 2 inside/outside (bppm) passes" if a.bppm else "",
                            a.length, W),
             "fold": a.fold,
+            "bppm": a.bppm,
             "walkers_per_gpu": W,
             "global_walkers": W * world,
             "length": a.length,
@@ -219,7 +230,7 @@ def main():
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds, a.fold)
+        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds, a.fold, terms)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

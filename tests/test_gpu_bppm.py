@@ -28,10 +28,10 @@ def rand_seq(rng, n):
 def test_fold_bpp_matches_oracle(native, oracle):
     rng = random.Random(23)
     cases = [("GGGGAAACCCC", None), ("ACGUGAAAACGU", "((((....))))"), (workloads.THEO_SEQ, None)]
-    for n in (20, 45, 80, 100):
+    for n in (20, 45, 80, 100, 150):
         for _ in range(2):
             cases.append((rand_seq(rng, n), None))
-    cases.append((cases[-1][0], "." * 10 + "x" * 5 + "." * 85))
+    cases.append((cases[-3][0], "." * 10 + "x" * 5 + "." * 85))
     for seq, cst in cases:
         f = native.Fold(seq)
         if cst:
@@ -71,7 +71,7 @@ def _oracle_sf(oracle, terms, contexts=None):
     return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts)
 
 
-@pytest.mark.parametrize("N", [60, 100])
+@pytest.mark.parametrize("N", [60, 100, 150])
 def test_bppm_batch(native, oracle, N):
     tmpl, active = workloads.synthetic(N)
     eng = _engine(native, tmpl, [active], _objective(N))
@@ -91,7 +91,7 @@ def _close_term(a, b):
     return abs(a - b) <= 2e-3 or abs(math.exp(a) - math.exp(b)) <= P_TOL
 
 
-@pytest.mark.parametrize("N", [60, 100])
+@pytest.mark.parametrize("N", [60, 100, 150])
 def test_score_with_pair_terms(native, oracle, N):
     tmpl, active = workloads.synthetic(N)
     terms = _objective(N)
