@@ -425,7 +425,16 @@ __device__ __forceinline__ void qb_terms_dispatch(int sS, int sG, const Lds<P> &
 }
 
 // ---------------------------------------------------------------- work split
-// Per-diagonal item counts and estimated costs (x4 units) of iteration d.
+// Per-diagonal item counts and estimated costs of iteration d (units ~8 cycles).
+#ifndef ADX_CA0
+#define ADX_CA0 50
+#endif
+#ifndef ADX_CB1
+#define ADX_CB1 16
+#endif
+#ifndef ADX_CB0
+#define ADX_CB0 16
+#endif
 struct RangeCost {
     int cp, cq, umax, nS, nG, sS, sG, nit, sQ5, cqg, ca, cb, c5, Ct;
 };
@@ -445,9 +454,12 @@ __host__ __device__ inline RangeCost range_cost(int d, int N, int cp) {
     r.nit = r.cq ? (sq - 3 + 15) / 16 : 0;                  // qm: 16 lanes per cell
     r.sQ5 = (d - 4 + WAVE - 1) / WAVE;
     r.cqg = (r.cq + 3) / 4;                                 // qm items = groups of 4 cells
-    r.ca = (4 * r.sG + 12 * r.sS) * (P + 1) / 2 + 16;
-    r.cb = 6 * r.nit * P + 12;
-    r.c5 = 16 * r.sQ5 + 16;
+    // weights calibrated on per-phase cycle stamps (tools/pf_stamps.py, N = 100,
+    // P = 2): ~8 cycles per unit; a closing-pair cell also pays ~210 cycles of
+    // chunk set-up, a qm group ~40 + 40 per 16-split step, q5 ~320 per slot
+    r.ca = (4 * r.sG + 12 * r.sS) * (P + 1) / 2 + ADX_CA0;
+    r.cb = (ADX_CB1 * r.nit + ADX_CB0) * P;
+    r.c5 = 40 * r.sQ5 + 40;
     r.Ct = r.c5 + r.cp * r.ca + r.cqg * r.cb;
     return r;
 }

@@ -15,10 +15,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--W", type=int, default=4096)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--N", type=int, default=100)
+ap.add_argument("--fold", default="pf")
 a = ap.parse_args()
 tmpl, active = workloads.synthetic(a.N)
 apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
-eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt)
+eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt, fold_mode=a.fold)
 seqs = workloads.walker_sequences(tmpl, [active], a.W)
 one = []
 for _ in range(a.reps):

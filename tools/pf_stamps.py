@@ -10,8 +10,9 @@ from addapt_amd import native, workloads  # noqa: E402
 L = native.lib()
 L.adx_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 tmpl, active = workloads.synthetic(int(sys.argv[1]) if len(sys.argv) > 1 else 100)
+fold = sys.argv[2] if len(sys.argv) > 2 else "pf"
 apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
-eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt)
+eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt, fold_mode=fold)
 buf = (C.c_ulonglong * 256)()
 eng.score_batch([tmpl])
 L.adx_debug_stamps(buf, 1)
