@@ -1084,7 +1084,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
 }
 
 template <int NT, int P, class SR>
-__global__ void __launch_bounds__(NT, (NT == 768) ? 3 : 4)
+__global__ void __launch_bounds__(NT, (P == 2) ? (NT > 512 ? 3 : 2) : 4)   // min waves per SIMD
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
