@@ -418,6 +418,11 @@ struct Problem {
     DevBuf<int> dBvars, dPairs;
     DevBuf<double> dPairP;
     DevBuf<char> dScratch;       // outside tables in HBM when they do not fit LDS
+    // MFE: packed 16-bit copies of the energy tables (kernels.hip MinPlus16)
+    DevBuf<DevTables> dT16;
+    DevBuf<DevScaled> dX16;
+    DevBuf<int> dOvf;
+    bool mfe16 = false;
     std::unique_ptr<DevTables> hT;
     std::unique_ptr<DevScaled> hX;
 
@@ -466,6 +471,9 @@ struct Problem {
         ka.n_pairs = static_cast<int>(pairs.size() / 3);
         ka.pair_p = dPairP.p;
         ka.bppm_scratch = dScratch.p;
+        ka.T16 = mfe16 ? dT16.p : nullptr;
+        ka.X16 = mfe16 ? dX16.p : nullptr;
+        ka.ovf = mfe16 ? dOvf.p : nullptr;
         return ka;
     }
 
@@ -486,6 +494,45 @@ struct Problem {
     adx_status upload_scaled() {
         build_scaled(*P, sigma(), motif, motif_eint, motif_pt, *hX, mode == 1);
         HIP_TRY(dX.upload(hX.get(), 1, stream));
+        return ADX_OK;
+    }
+
+    // MFE: the energy tables as packed int16 pairs (value duplicated in both
+    // halves; >= MFE_BIG/2 -> 0x7FFF).  Returns false when a value does not fit.
+    static bool pack16(float *a, size_t n) {
+        for (size_t k = 0; k < n; k++) {
+            const double e = a[k];
+            uint32_t h;
+            if (e >= 0.5 * MFE_BIG) h = 0x7FFFu;
+            else if (e <= -16384.0 || e >= 16384.0 || e != std::floor(e)) return false;
+            else h = static_cast<uint16_t>(static_cast<int16_t>(e));
+            const uint32_t w = h | (h << 16);
+            std::memcpy(&a[k], &w, 4);
+        }
+        return true;
+    }
+    adx_status upload_mfe16() {
+        mfe16 = false;
+        if (mode != 1 || std::getenv("ADX_NO_MFE16")) return ADX_OK;
+        auto T16 = std::make_unique<DevTables>(*hT);
+        auto X16 = std::make_unique<DevScaled>(*hX);
+        bool ok = pack16(reinterpret_cast<float *>(T16.get()), sizeof(DevTables) / sizeof(float));
+        ok = ok && pack16(X16->ctab, CT_SIZE) && pack16(X16->fgen, FG_SIZE) && pack16(X16->s_f, NS_MAX) &&
+             pack16(X16->g_f, NG_MAX) && pack16(X16->sig, NMAX + 4) && pack16(X16->hp, NMAX + 1) &&
+             pack16(X16->pwml, NMAX + 1) && pack16(&X16->mlclosing, 1) && pack16(&X16->mlbase_sig, 1) &&
+             pack16(X16->sp_val, MAX_SPECIAL_HP) && pack16(&X16->motif_extra, 1);
+        if (!ok) return ADX_OK;   // FP32 MinPlus only
+        HIP_TRY(dT16.upload(T16.get(), 1, stream));
+        HIP_TRY(dX16.upload(X16.get(), 1, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        mfe16 = true;
+        return ADX_OK;
+    }
+    adx_status ensure_ovf(int W) {
+        if (mfe16 && dOvf.n < size_t(W)) {
+            HIP_TRY(dOvf.alloc(W));
+            HIP_TRY(hipMemsetAsync(dOvf.p, 0, sizeof(int) * W, stream));
+        }
         return ADX_OK;
     }
 
@@ -524,6 +571,8 @@ struct Problem {
         HIP_TRY(dBvars.upload(bvars.data(), bvars.size(), stream));
         HIP_TRY(dPairs.upload(pairs.data(), pairs.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        s = upload_mfe16();
+        if (s) return s;
         if (!pairs.empty() && bppm_lds_bytes(kargs(), nullptr) == 0)
             return fail(ADX_EUNSUPPORTED, "base-pair probabilities of length %d do not fit one CU's LDS yet", Nmax);
         return choose_layout();
@@ -543,6 +592,8 @@ struct Problem {
 
     // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
     adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
+        adx_status so = ensure_ovf(W);
+        if (so) return so;
         if (!pairs.empty()) {
             adx_status s = ensure_pairs(W);
             if (s) return s;

@@ -148,6 +148,11 @@ struct KArgs {
     int n_pairs;
     const double *pair_p;       // [W][n_pairs] probabilities written by bppm_kernel (score input)
     char *bppm_scratch;         // global outside tables when they do not fit LDS (N >~ 110)
+    // MFE: packed 16-bit tables (two variants per value) and the per-walker flag of
+    // folds that left the 16-bit exact range (re-folded with the FP32 tables T, X)
+    const DevTables *T16;
+    const DevScaled *X16;
+    int *ovf;
 };
 
 // Monte Carlo state (device, read/write).

@@ -60,6 +60,7 @@ __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlan
 // for SumProd and MARK for MinPlus.
 struct SumProd {
     static constexpr bool MFE = false;
+    static constexpr int NV = 1;   // variants per value
     __device__ static float zero() { return 0.f; }
     __device__ static float one() { return 1.f; }
     __device__ static float add(float a, float b) { return a + b; }
@@ -71,6 +72,7 @@ struct SumProd {
 };
 struct MinPlus {
     static constexpr bool MFE = true;
+    static constexpr int NV = 1;
     __device__ static float zero() { return MFE_BIG; }
     __device__ static float one() { return 0.f; }
     __device__ static float add(float a, float b) { return fminf(a, b); }
@@ -80,6 +82,57 @@ struct MinPlus {
     __device__ static bool is_mark(float x) { return x == MFE_MARK; }
     __device__ static float fin(float x) { return fminf(x, MFE_BIG); }   // never MARK
 };
+
+// Packed 16-bit min-plus: TWO variants per 32-bit value (the apo and holo folds
+// of one group in the low / high half), v_pk_add_i16 (saturating) and
+// v_pk_min_i16, so one instruction advances both folds and the tables take
+// half the LDS of the FP32 pair.  Values travel in float registers as raw bits
+// (only moves, selects and these ops touch them).  Encoding per half: integer
+// dcal/mol; 0x7FFF = impossible; any value >= 0x4000 counts as impossible and
+// is reset to 0x7FFF when a cell is stored (fin).  Exact while every stored
+// value stays >= MFE16_FLOOR (checked at the end of the fold; a walker that
+// fails the check is re-folded by the FP32 MinPlus kernel).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+constexpr int MFE16_FLOOR = -12000;
+struct MinPlus16 {
+    static constexpr bool MFE = true;
+    static constexpr int NV = 2;
+    __device__ static s16x2 v(float x) { return __builtin_bit_cast(s16x2, x); }
+    __device__ static float f(s16x2 x) { return __builtin_bit_cast(float, x); }
+    __device__ static float zero() { return __uint_as_float(0x7FFF7FFFu); }
+    __device__ static float one() { return 0.f; }
+    __device__ static float add(float a, float b) { return f(__builtin_elementwise_min(v(a), v(b))); }
+    __device__ static float mul(float a, float b) { return f(__builtin_elementwise_add_sat(v(a), v(b))); }
+    __device__ static float fma(float a, float b, float c) { return add(mul(a, b), c); }
+    __device__ static float mark() { return __uint_as_float(0x7FFE7FFEu); }
+    __device__ static bool is_mark(float x) { return __float_as_uint(x) == 0x7FFE7FFEu; }
+    __device__ static float fin(float x) {   // halves in [0x4000, 0x7FFF] -> 0x7FFF
+        const uint32_t u = __float_as_uint(x);
+        const uint32_t imp = (u & ~(u >> 1)) & 0x40004000u;
+        return __uint_as_float(u | ((imp >> 14) * 0x7FFFu));
+    }
+};
+
+// Loop-factor selectors of qb_terms (0/1 selector floats from the term lists):
+// the outer-pair factor of a slot-0 term, the prefetched table factor, and the
+// slot-1 choice between the 1xn and bulge outer factor.
+template <class SR>
+__device__ __forceinline__ float sel_outer(float eb, float em, float e3, float tau, float mo, float m23) {
+    if constexpr (SR::NV == 2)
+        return eb != 0.f ? tau : (em != 0.f ? mo : (e3 != 0.f ? m23 : SR::one()));
+    const float one = SR::one();
+    return fmaf(eb, tau - one, fmaf(em, mo - one, fmaf(e3, m23 - one, one)));
+}
+template <class SR>
+__device__ __forceinline__ float sel_tab(float eg, float gtab) {
+    if constexpr (SR::NV == 2) return eg != 0.f ? gtab : SR::one();
+    return fmaf(eg, gtab - SR::one(), SR::one());
+}
+template <class SR>
+__device__ __forceinline__ float sel2(float em1, float mo, float tau) {
+    if constexpr (SR::NV == 2) return em1 != 0.f ? mo : tau;
+    return fmaf(em1, mo - tau, tau);
+}
 
 // Full-wave reductions via DPP (quad_perm, row_shr, row_bcast): VALU-only, no
 // LDS crossbar.  Lanes a DPP move does not write keep the identity (SR::zero).
@@ -369,11 +422,10 @@ __device__ __forceinline__ void qb_terms(const Lds<P> &L, const TermLanes &D, co
     // slot 0: stack / bulge 1 / 1x1..2x2 tables / 2x3 / bulges / 1xn.  uf and gf
     // select (0/1 selectors, one per kind) the outer-pair factor and the
     // prefetched table factor, or the semiring one.
-    const float one = SR::one();
     const int t2 = (c0 * 41) >> 10;
     const int i2 = D.b2 + ((u.ty8 + t2) & D.mwt) + (c0 & D.mwc);
-    const float uf = fmaf(D.eb, u.tau - one, fmaf(D.em, u.mo - one, fmaf(D.e3, u.m23 - one, one)));
-    const float gf = fmaf(D.eg, gtab - one, one);
+    const float uf = sel_outer<SR>(D.eb, D.em, D.e3, u.tau, u.mo, u.m23);
+    const float gf = sel_tab<SR>(D.eg, gtab);
     float f0 = SR::mul(SR::mul(SR::mul(ct[D.b1[0] + c0], ct[i2]), SR::mul(D.fS[0], uf)), gf);
     if (MK) {
         const int pk = int(L.sd[lane]);
@@ -382,7 +434,7 @@ __device__ __forceinline__ void qb_terms(const Lds<P> &L, const TermLanes &D, co
     float f1 = SR::zero();
     if (SS > 1) {
         // slot 1: bulges and 1xn only
-        f1 = SR::mul(ct[D.b1[1] + c1], SR::mul(D.fS[1], fmaf(D.em1, u.mo - u.tau, u.tau)));
+        f1 = SR::mul(ct[D.b1[1] + c1], SR::mul(D.fS[1], sel2<SR>(D.em1, u.mo, u.tau)));
         if (MK) {
             const int pk = int(L.sd[WAVE + lane]);
             f1 = ((pk & 255) <= u.A && ((pk >> 8) & 255) <= u.B) ? f1 : SR::zero();
@@ -500,12 +552,21 @@ __device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
 // ranges of equal estimated cost, one per wave.
 template <int NT, int P, class SR>
 __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, const Lds<P> &L,
-                         const DevScaled *__restrict__ XS, float (&z)[P]) {
+                         const DevScaled *__restrict__ XS, float (&z)[P], bool &bad) {
     constexpr int NW = NT / WAVE;
     const DevVariant V = ka.variants[vs[0]];
+    // motif[p]: table p carries a holo variant; NV = 2 packs variants vs[2p], vs[2p+1]
     bool motif[P];
+    bool mhalf[2] = {false, false};
 #pragma unroll
-    for (int p = 0; p < P; p++) motif[p] = ka.variants[vs[p]].motif != 0;
+    for (int p = 0; p < P; p++) {
+        motif[p] = false;
+        for (int h = 0; h < SR::NV; h++) {
+            const bool m = ka.variants[vs[p * SR::NV + h]].motif != 0;
+            motif[p] |= m;
+            mhalf[h] = m;
+        }
+    }
     const int N = uni(V.N);
     const float *ct = L.ct;
     const int tid = threadIdx.x;
@@ -545,6 +606,10 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 #pragma unroll
     for (int p = 0; p < P; p++)
         for (int k = tid; k < 2 * NP; k += NT) L.mla[p][k] = SR::zero();
+    if constexpr (SR::NV == 2) {   // qm spans N-2, N-1 are never computed: defined for the range guard
+        const int C = ((N - 4) * (N - 3)) >> 1;
+        for (int k = tid; k < C; k += NT) L.qm[0][k] = SR::zero();
+    }
     constrained = __syncthreads_or(constrained);
     if (tid == 0) {
         // ViennaRNA's S1 wrap-around (only reaches values that are never used)
@@ -574,7 +639,11 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     const float mlbase_sig = XS->mlbase_sig;
     const float mlclosing = XS->mlclosing;
     const float eTAU = XS->ctab[CT_FSM + 6];
-    const float mextra = XS->motif_extra;
+    // packed values: the motif term applies to the holo half only (0x7FFF = no-op for min)
+    const float mextra = SR::NV == 2
+        ? __uint_as_float((mhalf[0] ? (__float_as_uint(XS->motif_extra) & 0xFFFFu) : 0x7FFFu) |
+                          (mhalf[1] ? (__float_as_uint(XS->motif_extra) & 0xFFFF0000u) : 0x7FFF0000u))
+        : XS->motif_extra;
     const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
     if (tid == 0) {
 #pragma unroll
@@ -1016,6 +1085,23 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 #endif
 #pragma unroll
     for (int p = 0; p < P; p++) z[p] = L.q5[p][N];   // scaled Z; energies after the group loop
+    bad = false;
+    if constexpr (SR::NV == 2) {
+        // exactness guard of the 16-bit encoding (MinPlus16): every stored value >= floor
+        bool low = false;
+        const int C = ((N - 4) * (N - 3)) >> 1;
+        auto chk = [&](float x) {
+            const s16x2 q = MinPlus16::v(x);
+            low |= (q.x < MFE16_FLOOR) || (q.y < MFE16_FLOOR);
+        };
+        for (int k = tid; k < C; k += NT) {
+            chk(L.qbm[0][k]);
+            chk(L.qm[0][k]);
+            chk(L.qm1[0][k]);
+        }
+        for (int k = tid; k <= N; k += NT) chk(L.q5[0][k]);
+        bad = __syncthreads_or(low);
+    }
 }
 
 // ---------------------------------------------------------------- scoring
@@ -1048,21 +1134,30 @@ __device__ double combine_score(const KArgs &ka, const Lds<P> &L, const double *
 template <int NT, int P, class SR>
 __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
                                  const uint8_t *raw, const Lds<P> &L, const double *pp,
-                                 float *dG_out, double *terms_out) {
-    const int ng = P == 2 ? ka.n_groups2 : ka.n_variants;
+                                 float *dG_out, double *terms_out, bool &any_bad) {
+    const int ng = P * SR::NV == 2 ? ka.n_groups2 : ka.n_variants;
+    any_bad = false;
     for (int g = 0; g < ng; g++) {
-        int vs[P];
-        if constexpr (P == 2) {
+        int vs[P * SR::NV];
+        if constexpr (P * SR::NV == 2) {
             vs[0] = ka.groups2[2 * g];
             vs[1] = ka.groups2[2 * g + 1];
         } else {
             vs[0] = g;
         }
         float z[P];
-        pf_group<NT, P, SR>(ka, vs, raw, L, XS, z);
+        bool bad = false;
+        pf_group<NT, P, SR>(ka, vs, raw, L, XS, z, bad);
+        any_bad |= bad;
         if (threadIdx.x == 0) {
+            if constexpr (SR::NV == 2) {
+                const s16x2 q = MinPlus16::v(z[0]);
+                L.G[vs[0]] = (q.x >= 0x4000) ? double(MFE_BIG) : static_cast<double>(q.x);
+                L.G[vs[1]] = (q.y >= 0x4000) ? double(MFE_BIG) : static_cast<double>(q.y);
+            } else {
 #pragma unroll
-            for (int p = 0; p < P; p++) L.G[vs[p]] = static_cast<double>(z[p]);
+                for (int p = 0; p < P; p++) L.G[vs[p]] = static_cast<double>(z[p]);
+            }
         }
         __syncthreads();   // the next group rewrites the tables
     }
@@ -1084,7 +1179,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
 }
 
 template <int NT, int P, class SR>
-__global__ void __launch_bounds__(NT, (P == 2) ? (NT > 512 ? 3 : 2) : 4)   // min waves per SIMD
+__global__ void __launch_bounds__(NT, (NT > 512) ? 3 : (P == 2 ? 2 : 4))   // min waves per SIMD
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1092,15 +1187,20 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, (ka.opt & 1) != 0, (ka.opt & 2) != 0);
     const int w = blockIdx.x;
     if (w >= W) return;
+    if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
     if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
     load_ctab(ka, L);
     for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
     __syncthreads();
     const int nt = ka.n_terms * ka.n_ctx_eff;
     const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
+    bool bad = false;
     const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, pp, dG ? dG + size_t(w) * ka.n_variants : nullptr,
-                                          terms ? terms + size_t(w) * nt : nullptr);
-    if (threadIdx.x == 0) scores[w] = s;
+                                          terms ? terms + size_t(w) * nt : nullptr, bad);
+    if (threadIdx.x == 0) {
+        scores[w] = s;
+        if (SR::NV == 2 && bad && ka.ovf) ka.ovf[w] = 1;   // re-folded by the FP32 MinPlus kernel
+    }
 }
 
 // ---------------------------------------------------------------- outside / bppm
@@ -1408,7 +1508,8 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
     const int v = ka.bvars[bv];
     const int vs[1] = {v};
     float z[1];
-    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z);
+    bool bad = false;
+    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z, bad);
     __syncthreads();
     outside<NT>(ka, v, bv, L, O, XS, z[0],
                 full ? full + (size_t(w) * ka.n_bvars + bv) * size_t(ld) * ld : nullptr, ld,
@@ -1630,6 +1731,9 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 #ifndef ADX_NT2
 #define ADX_NT2 768     // 12 waves x 168 VGPRs (16 x 128 spills)
 #endif
+#ifndef ADX_NT16
+#define ADX_NT16 512    // packed 16-bit MFE
+#endif
 template <int P>
 static size_t lds_size(const KArgs &ka, bool pl, bool rt) {
     return lds_layout<true, P>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, pl, rt);
@@ -1646,8 +1750,12 @@ static int choose_p(const KArgs &ka) {
 template <int P>
 static void choose_opt(const KArgs &ka, bool &pl, bool &rt) {
     // P = 1 keeps two workgroups per CU when they fit (1 KiB margin for allocation granularity)
+#ifdef ADX_1WG
+    const size_t lim = LDS_LIMIT;
+#else
     const size_t lim = (P == 1 && 2 * lds_size<1>(ka, false, false) <= size_t(LDS_LIMIT) - 2048)
                            ? LDS_LIMIT / 2 - 1024 : LDS_LIMIT;
+#endif
     rt = lds_size<P>(ka, false, true) <= lim;
     pl = lds_size<P>(ka, true, rt) <= lim;
 #ifdef ADX_NO_OPT
@@ -1688,6 +1796,18 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
 hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
                           float *dG, const int *mask, hipStream_t stream) {
     // ka.mode: 0 = partition functions (vrna_pf), 1 = minimum free energies
+    if (ka.mode == 1 && ka.X16 && ka.ovf) {
+        // packed 16-bit folds (two variants per value, two workgroups per CU), then
+        // the FP32 MinPlus kernel for the walkers whose values left the exact range
+        KArgs k16 = ka;
+        k16.T = ka.T16;
+        k16.X = ka.X16;
+        hipError_t e = launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
+        if (e != hipSuccess) return e;
+        if (choose_p(ka) == 2)
+            return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, ka.ovf, stream);
+        return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, ka.ovf, stream);
+    }
     if (ka.mode == 1) {
         if (choose_p(ka) == 2)
             return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);

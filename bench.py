@@ -181,7 +181,7 @@ def main():
         if a.fold == "pf" else
         ("fp32 VALU add/min on integer dcal energies (min-plus is not an MFMA contraction); "
          "peak = gfx950 fp32 rate"),
-        "kernel": "score_kernel<%s>" % ("MinPlus" if a.fold == "mfe" else "SumProd"),
+        "kernel": "score_kernel<%s>" % ("MinPlus16 (+ FP32 MinPlus fallback)" if a.fold == "mfe" else "SumProd"),
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": score_ms,
         "launches": launches,

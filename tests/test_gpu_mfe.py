@@ -61,6 +61,39 @@ def test_fold_mfe_matches_oracle(native, oracle):
         assert _same(g, ref), (seq, cst, g, ref)
 
 
+def test_fold_mfe_extreme_energies(native, oracle):
+    """Folds far below the 16-bit path's exact range (-120 kcal/mol) take the FP32
+    fallback and stay bit-exact."""
+    for seq in ("G" * 70 + "AAAA" + "C" * 70, "GC" * 40 + "UUUU" + "GC" * 30, "GGGGCCCC" * 18):
+        f = native.Fold(seq)
+        g = f.mfe()
+        ref = oracle.mfe_energy(seq)
+        assert ref < -100.0
+        assert _same(g, ref), (seq, g, ref)
+
+
+def test_score_batch_mfe_mixed_fallback(native, oracle):
+    """A batch mixing ordinary walkers and GC-rich ones: per-walker fallback."""
+    tmpl, active = workloads.synthetic(150)
+    terms = workloads.default_objective()
+    eng = _engine(native, tmpl, [active], terms)
+    seqs = workloads.walker_sequences(tmpl, [active], 8)
+    o = (150 - 27) // 2
+    for w in (1, 6):   # GC-rich mutable bases, enforced-helix complements kept
+        s = list(seqs[w])
+        for i, c in enumerate(s):
+            if c.isupper() and 6 <= i < 144 and not (o - 6 <= i < o + 33):
+                s[i] = "G" if i < 75 else "C"
+        seqs[w] = "".join(s)
+    sc, tv, dg = eng.score_batch(seqs)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(8):
+            ref = oracle.mfe_energy(seqs[w], active if mac >= 0 else None, motif if cond == 1 else None)
+            assert _same(dg[w, v], ref), (v, w, dg[w, v], ref)
+
+
 def test_fold_mfe_motif(native, oracle):
     apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
     e = oracle.theo_bonus()
