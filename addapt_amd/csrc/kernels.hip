@@ -215,11 +215,13 @@ struct Lds {
     float *q5[P];
     uint8_t *cc;       // inner-pair code per cell (diagonal-major), shared
     uint8_t *pcnt;     // [d] pairable cells of diagonal d, shared
-    uint8_t *wsc;      // [wave][64] i of the cells of a wave's chunk
-    uint32_t *rec;     // optional (null when it does not fit): per pairable cell, by diagonal and rank:
-                       //   i | oc << 8 | up[i+1] << 16 | dn[j-1] << 24,  oc = type*25 + S[i+1]*5 + S[j-1]
+    uint8_t *wsc;      // without rec: [wave][64] i of the cells of a wave's chunk
+    uint8_t *rec;      // optional (null when it does not fit): i of every pairable cell, by
+                       //   diagonal and rank
+    uint32_t *rec32;   // optional, instead of rec when it fits: the full record word
+                       //   i | oc << 8 | up[i+1] << 16 | dn[j-1] << 24 (see load_chunk)
     uint16_t *rbase;   // with rec: first record of diagonal d
-    uint32_t *rt;      // optional: rt[d * 16 + w] = kb_lo | kb_hi << 8 | km_lo << 16 | km_hi << 24
+    uint32_t *rt;      // optional: rt[d * NW + w] = kb_lo | kb_hi << 8 | km_lo << 16 | km_hi << 24
     float *ct;         // CT_SIZE factor table (DevScaled::ctab)
     float *dt;         // per-cell tables (DT_*)
     uint16_t *gd;      // G list: n1 | n2 << 8        (NG_MAX)
@@ -236,7 +238,8 @@ struct Lds {
 // the pointers stay in the LDS address space)
 template <bool DRY, int P>
 __host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, int nvar, Lds<P> *L,
-                                             bool with_pl = false, bool with_rt = false) {
+                                             int pl_mode = 0, bool with_rt = false, int nw = 16) {
+    // pl_mode: 0 no record array, 1 rec (bytes), 2 rec32 (words)
     size_t o = 0;
     auto take = [&](size_t bytes) -> char * {
         char *p = DRY ? nullptr : base + o;
@@ -255,7 +258,7 @@ __host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, in
     }
     l.cc = reinterpret_cast<uint8_t *>(take(C));
     l.pcnt = reinterpret_cast<uint8_t *>(take(NP));
-    l.wsc = reinterpret_cast<uint8_t *>(take(16 * WAVE));
+    l.wsc = pl_mode ? nullptr : reinterpret_cast<uint8_t *>(take(16 * WAVE));
     l.ct = reinterpret_cast<float *>(take(CT_SIZE * 4));
     l.dt = reinterpret_cast<float *>(take(size_t(DT_HP + Nmax + 1) * 4));
     l.gd = reinterpret_cast<uint16_t *>(take(NG_MAX * 2));
@@ -274,9 +277,11 @@ __host__ __device__ inline size_t lds_layout(char *base, int cells, int Nmax, in
     l.raw = reinterpret_cast<uint8_t *>(take(NP));
     // pairable cells (i, j), j - i >= 4: S[i] and S[j] sit on opposite sides of the
     // bipartite pairing graph {A,G} x {C,U}, so there are at most N^2/4 of them
-    l.rec = with_pl ? reinterpret_cast<uint32_t *>(take((size_t(Nmax) * Nmax / 4 + Nmax) * 4)) : nullptr;
-    l.rbase = with_pl ? reinterpret_cast<uint16_t *>(take(size_t(NP) * 2)) : nullptr;
-    l.rt = with_rt ? reinterpret_cast<uint32_t *>(take(size_t(NP) * 16 * 4)) : nullptr;
+    const size_t nrec = size_t(Nmax) * Nmax / 4 + Nmax;
+    l.rec = pl_mode == 1 ? reinterpret_cast<uint8_t *>(take(nrec)) : nullptr;
+    l.rec32 = pl_mode == 2 ? reinterpret_cast<uint32_t *>(take(nrec * 4)) : nullptr;
+    l.rbase = pl_mode ? reinterpret_cast<uint16_t *>(take(size_t(NP) * 2)) : nullptr;
+    l.rt = with_rt ? reinterpret_cast<uint32_t *>(take(size_t(NP) * nw * 4)) : nullptr;
     l.np = NP;
     if (!DRY) *L = l;
     return o;
@@ -698,7 +703,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         if (lane == 0) L.pcnt[dd] = static_cast<uint8_t>(base);
     }
     __syncthreads();
-    if (L.rec) {
+    const bool has_rec = L.rec || L.rec32;
+    if (has_rec) {
         // record offsets: exclusive prefix sum of pcnt over the diagonals (wave 0)
         if (wid == 0) {
             int carry = 0;
@@ -725,10 +731,15 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const bool pr = r < c && !SR::is_mark(L.qbm[0][od + r]);
                 const unsigned long long bm = __ballot(pr);
                 if (pr) {
+                    const int k = rb + base + __popcll(bm & ((1ull << lane) - 1ull));
                     const int i = r + 1, j = i + dd;
-                    const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
-                    L.rec[rb + base + __popcll(bm & ((1ull << lane) - 1ull))] =
-                        uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) | (uint32_t(L.dn[j - 1]) << 24);
+                    if (L.rec32) {
+                        const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+                        L.rec32[k] = uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) |
+                                     (uint32_t(L.dn[j - 1]) << 24);
+                    } else {
+                        L.rec[k] = static_cast<uint8_t>(i);
+                    }
                 }
                 base += __popcll(bm);
             }
@@ -741,10 +752,10 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             RangeCost rc = range_cost<P>(d, N, d <= N - 1 ? int(L.pcnt[d]) : 0);
             int r[4];
             wave_range<NW>(rc, w, r);
-            L.rt[d * 16 + w] = uint32_t(r[0]) | (uint32_t(r[1]) << 8) | (uint32_t(r[2]) << 16) | (uint32_t(r[3]) << 24);
+            L.rt[d * NW + w] = uint32_t(r[0]) | (uint32_t(r[1]) << 8) | (uint32_t(r[2]) << 16) | (uint32_t(r[3]) << 24);
         }
     }
-    if (L.rt || L.rec) __syncthreads();
+    if (L.rt || has_rec) __syncthreads();
 
     // ---------------- loop-carried state.  prep(d) runs at the end of
     // iteration d-1 (before its barrier) and fills everything iteration d needs
@@ -793,11 +804,21 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     // lanes c < nc: cell kc + c (rank among the pairable cells of diagonal d)
     auto load_chunk = [&](int d, int kc, int nc) {
         const int od = off(d, N);
-        uint32_t wc, wp;   // record words of cell `lane` and of cell `lane / 4` of the chunk
-        if (L.rec) {
+        uint32_t wc, wp;   // record words of cell `lane` and of cell `lane / 4` of the chunk:
+                           //   i | oc << 8 | up[i+1] << 16 | dn[j-1] << 24, oc = type*25 + S[i+1]*5 + S[j-1]
+        auto word = [&](int i) {
+            const int j = i + d;
+            const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+            return uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) | (uint32_t(L.dn[j - 1]) << 24);
+        };
+        if (L.rec32) {
             const int rb = L.rbase[d] + kc;
-            wc = L.rec[rb + (lane < nc ? lane : nc - 1)];
-            wp = L.rec[rb + ((lane >> 2) < nc ? (lane >> 2) : nc - 1)];
+            wc = L.rec32[rb + (lane < nc ? lane : nc - 1)];
+            wp = L.rec32[rb + ((lane >> 2) < nc ? (lane >> 2) : nc - 1)];
+        } else if (L.rec) {
+            const int rb = L.rbase[d] + kc;
+            wc = word(L.rec[rb + (lane < nc ? lane : nc - 1)]);
+            wp = word(L.rec[rb + ((lane >> 2) < nc ? (lane >> 2) : nc - 1)]);
         } else {   // ballot scan of the non-pairable mark -> ws[rank - kc] = i
             int base = 0;
             for (int r0 = 0; r0 < N - d && base < kc + nc; r0 += WAVE) {
@@ -811,11 +832,6 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            auto word = [&](int i) {
-                const int j = i + d;
-                const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
-                return uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) | (uint32_t(L.dn[j - 1]) << 24);
-            };
             wc = word(ws[lane < nc ? lane : nc - 1]);
             wp = word(ws[(lane >> 2) < nc ? (lane >> 2) : nc - 1]);
         }
@@ -870,7 +886,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         sQ5 = rc.sQ5;
         const int nS = rc.nS, nG = rc.nG;
         if (L.rt) {
-            const uint32_t e = uni(int(L.rt[d * 16 + wid]));
+            const uint32_t e = uni(int(L.rt[d * NW + wid]));
             kb_lo = e & 255;
             kb_hi = (e >> 8) & 255;
             km_lo = (e >> 16) & 255;
@@ -1184,7 +1200,7 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<P> L;
-    lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, (ka.opt & 1) != 0, (ka.opt & 2) != 0);
+    lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, ka.opt & 3, (ka.opt & 4) != 0, NT / WAVE);
     const int w = blockIdx.x;
     if (w >= W) return;
     if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
@@ -1495,7 +1511,7 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
             double *full, int ld, double *pair_p, char *gscratch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<1> L;
-    const size_t o = lds_layout<false, 1>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, false, false);
+    const size_t o = lds_layout<false, 1>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, 0, false);
     Outs O;
     outs_layout<false, GOUT>(smem, o, ka.cells, ka.Nmax, &O,
                              GOUT ? gscratch + size_t(blockIdx.x) * outs_global_bytes(ka.cells) : nullptr);
@@ -1734,37 +1750,39 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 #ifndef ADX_NT16
 #define ADX_NT16 512    // packed 16-bit MFE
 #endif
-template <int P>
-static size_t lds_size(const KArgs &ka, bool pl, bool rt) {
-    return lds_layout<true, P>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, pl, rt);
+template <int P, int NT = (P == 2 ? ADX_NT2 : 512)>
+static size_t lds_size(const KArgs &ka, int pl, bool rt) {
+    return lds_layout<true, P>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, pl, rt, NT / WAVE);
 }
 
 static int choose_p(const KArgs &ka) {
 #ifdef ADX_FORCE_P1
     return 1;
 #endif
-    return lds_size<2>(ka, false, false) <= size_t(LDS_LIMIT) ? 2 : 1;
+    return lds_size<2>(ka, 0, false) <= size_t(LDS_LIMIT) ? 2 : 1;
 }
 
 // optional LDS arrays (rank list, range table) when they still fit
-template <int P>
-static void choose_opt(const KArgs &ka, bool &pl, bool &rt) {
+template <int P, int NT = (P == 2 ? ADX_NT2 : 512)>
+static void choose_opt(const KArgs &ka, int &pl, bool &rt) {
     // P = 1 keeps two workgroups per CU when they fit (1 KiB margin for allocation granularity)
 #ifdef ADX_1WG
     const size_t lim = LDS_LIMIT;
 #else
-    const size_t lim = (P == 1 && 2 * lds_size<1>(ka, false, false) <= size_t(LDS_LIMIT) - 2048)
+    const size_t lim = (P == 1 && 2 * lds_size<1, NT>(ka, 0, false) <= size_t(LDS_LIMIT) - 2048)
                            ? LDS_LIMIT / 2 - 1024 : LDS_LIMIT;
 #endif
-    rt = lds_size<P>(ka, false, true) <= lim;
-    pl = lds_size<P>(ka, true, rt) <= lim;
+    rt = lds_size<P, NT>(ka, 0, true) <= lim;
+    pl = lds_size<P, NT>(ka, 2, rt) <= lim ? 2 : lds_size<P, NT>(ka, 1, rt) <= lim ? 1 : 0;
 #ifdef ADX_NO_OPT
-    pl = rt = false;
+    pl = 0;
+    rt = false;
 #endif
 }
 
 size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
-    bool pl, rt;
+    int pl;
+    bool rt;
     if (choose_p(ka) == 2) {
         choose_opt<2>(ka, pl, rt);
         return lds_size<2>(ka, pl, rt);
@@ -1776,9 +1794,10 @@ size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
 template <int NT, int P, class SR>
 static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
                                  float *dG, const int *mask, hipStream_t stream) {
-    bool pl, rt;
-    choose_opt<P>(ka, pl, rt);
-    const size_t lds = lds_size<P>(ka, pl, rt);
+    int pl;
+    bool rt;
+    choose_opt<P, NT>(ka, pl, rt);
+    const size_t lds = lds_size<P, NT>(ka, pl, rt);
     auto k = score_kernel<NT, P, SR>;
     static size_t configured = 0;
     if (lds > configured) {
@@ -1788,7 +1807,7 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
         configured = lds;
     }
     KArgs kb = ka;
-    kb.opt = (pl ? 1 : 0) | (rt ? 2 : 0);
+    kb.opt = pl | (rt ? 4 : 0);
     hipLaunchKernelGGL(k, dim3(W), dim3(NT), lds, stream, kb, kb.X, seqs, W, scores, terms, dG, mask);
     return hipGetLastError();
 }
@@ -1825,7 +1844,7 @@ hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, doubl
 // outside pass: LDS bytes of the all-LDS layout, or of the global-scratch
 // layout (gout = true) when that does not fit; 0 when neither fits one CU.
 size_t bppm_lds_bytes(const KArgs &ka, bool *gout) {
-    const size_t o = lds_layout<true, 1>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, false, false);
+    const size_t o = lds_layout<true, 1>(nullptr, ka.cells, ka.Nmax, ka.n_variants, nullptr, 0, false);
     const size_t t = outs_layout<true, false>(nullptr, o, ka.cells, ka.Nmax, nullptr);
     if (t <= size_t(LDS_LIMIT)) {
         if (gout) *gout = false;
