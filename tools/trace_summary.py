@@ -1,23 +1,33 @@
 #!/usr/bin/env python3
-"""Average duration of the timed MC-step score_kernel launches in a rocprofv3
-kernel trace (bench_kernel_trace.csv): the LAST `--last K` launches (K = the
-bench's --steps), i.e. the launches bench.py's roofline.kernel_ms_per_launch
-times with HIP events -- calibration, walkers_init and warmup launches are
-excluded.
+"""Per-step duration of the score kernel(s) in a rocprofv3 kernel trace
+(bench_kernel_trace.csv), comparable with bench.py's
+roofline.kernel_ms_per_launch (HIP events around each step's score launch,
+which for the MFE fold covers the packed 16-bit kernel and its FP32 fallback
+launch).  For every score_kernel instantiation the LAST `--last K` launches
+(K = the bench's --steps: calibration, walkers_init and warmup launches
+excluded) are averaged; the per-step figure is the sum over instantiations.
 
 usage: trace_summary.py bench_kernel_trace.csv [--last K]
 """
+import collections
 import csv
 import json
 import sys
 
 path = sys.argv[1]
 last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 10
-rows = [r for r in csv.DictReader(open(path)) if "score_kernel" in r["Kernel_Name"]]
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
-step = d[-last:]
-names = sorted({r["Kernel_Name"] for r in rows[-last:]})
-print(json.dumps({"score_kernel_launches": len(step), "avg_ms": sum(step) / len(step),
-                  "min_ms": min(step), "max_ms": max(step), "kernel_names": names,
-                  "selection": "last %d launches (the timed steps)" % last}, indent=1))
+by = collections.defaultdict(list)
+for r in csv.DictReader(open(path)):
+    if "score_kernel" in r["Kernel_Name"]:
+        by[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+out = {"selection": "last %d launches of each score_kernel instantiation (the timed steps)" % last,
+       "kernels": {}}
+per_step = 0.0
+for name, rows in by.items():
+    rows.sort()
+    d = [(e - s) / 1e6 for s, e in rows][-last:]
+    avg = sum(d) / len(d)
+    per_step += avg
+    out["kernels"][name] = {"launches": len(d), "avg_ms": avg, "min_ms": min(d), "max_ms": max(d)}
+out["avg_ms_per_step"] = per_step
+print(json.dumps(out, indent=1))
