@@ -78,14 +78,17 @@ double GpuRnaFold::base_pair_prob(int i, int j) const {
     const int n = static_cast<int>(seq_.size());
     if (i < 0 || j < 0 || i >= n || j >= n) throw string("base pair index out of range");
     if (i == j) return 0.0;
-    adx_fold *raw = nullptr;
-    gpu::check(adx_fold_create(gpu::params(), seq_.c_str(), 1, gpu_, &raw));
-    gpu::FoldPtr f(raw);
-    if (aptamer_)
-        gpu::check(adx_fold_add_motif(f.get(), aptamer_->seq().c_str(), aptamer_->fold().c_str(),
-                                      kT() * std::log(aptamer_->affinity() / 1e6)));
-    double p = 0.0;
-    gpu::check(adx_fold_bpp(f.get(), std::min(i, j) + 1, std::max(i, j) + 1, &p));
+    if (!bppm_fold_) {
+        adx_fold *raw = nullptr;
+        gpu::check(adx_fold_create(gpu::params(), seq_.c_str(), 1, gpu_, &raw));
+        std::shared_ptr<::adx_fold> f(raw, adx_fold_free);
+        if (aptamer_)
+            gpu::check(adx_fold_add_motif(f.get(), aptamer_->seq().c_str(), aptamer_->fold().c_str(),
+                                          kT() * std::log(aptamer_->affinity() / 1e6)));
+        bppm_fold_ = f;
+    }
+    double p = 0.0;   // the matrix is computed on the first call and cached by the fold
+    gpu::check(adx_fold_bpp(bppm_fold_.get(), std::min(i, j) + 1, std::max(i, j) + 1, &p));
     return p;
 }
 

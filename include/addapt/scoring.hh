@@ -13,6 +13,8 @@
 
 #include "addapt/model.hh"
 
+struct adx_fold;   // include/addapt_gpu.h (C ABI fold compound)
+
 namespace addapt {
 
 class ScoreFunction;
@@ -52,6 +54,8 @@ private:
     string seq_;
     AptamerConstPtr aptamer_;
     int gpu_;
+    // the bppm fold compound, built and folded on first use (scoring.cc:41-44)
+    mutable std::shared_ptr<::adx_fold> bppm_fold_;
 };
 using ViennaRnaFold = GpuRnaFold;   // the reference's name for this role
 

@@ -110,3 +110,29 @@ def test_cli_batched_walkers(oracle, tmp_path):
         assert float(f[2]) == pytest.approx(ref, abs=2e-3)
         # frozen (lower-case) positions never change
         assert all(a == b for a, b in zip(seq, workloads.RHF6_SEQ) if b.islower())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("holo", [False, True])
+def test_cpp_base_pair_prob_matches_oracle(oracle, tmp_path, holo):
+    """ViennaRnaFold::base_pair_prob of the C++ mirror (scoring.cc:37-51): one
+    outside pass on the first call, cached for the rest, against orc_bppm."""
+    lib = os.path.join(ROOT, "addapt_amd", "_lib")
+    exe = str(tmp_path / "bpp_probe")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "bpp_probe.cc"), "-L", lib, "-laddapt_host",
+                    "-laddapt_gpu", "-Wl,-rpath," + lib], check=True)
+    seq = "GGGA" + workloads.THEO_SEQ + "UCCCAAGGAUCC"
+    r = subprocess.run([exe, seq] + (["holo"] if holo else []), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0) if holo else None
+    _, ref = oracle.bppm(seq, None, m)
+    lines = r.stdout.split("\n")
+    for line in lines:
+        if not line or line.startswith("sym"):
+            continue
+        i, j, p = line.split()
+        assert abs(float(p) - ref[int(i), int(j)]) <= 2e-4, (i, j, p, ref[int(i), int(j)])
+    sym = [l for l in lines if l.startswith("sym")][0]
+    assert abs(float(sym.split()[1]) - ref[0, len(seq) - 1]) <= 2e-4
