@@ -1017,7 +1017,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             float sums[P];
 #pragma unroll
             for (int p = 0; p < P; p++) sums[p] = SR::zero();
-            for (int c = 0; c < nc; c++) {
+            // the interior-loop sums of one cell of the chunk (lanes = terms)
+            auto cell_terms = [&](int c, float (&part)[P]) {
                 CellU u;
                 u.i = __builtin_amdgcn_readlane(ci, c);
                 u.ty8 = __builtin_amdgcn_readlane(cty, c) * 8;
@@ -1030,7 +1031,6 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const bool masked = constrained && (u.A < umax || u.B < umax);
                 // gather of the prefetched 1x1..2x2 table factors for this cell
                 const float gtab = __shfl(pfx, c * 4 + D.gsel, WAVE);
-                float part[P], tot[P];
 #ifndef ADX_ABL_QBT
                 if (masked) qb_terms_dispatch<SR, true, P>(sS, sG, L, D, u, gtab, part);
                 else qb_terms_dispatch<SR, false, P>(sS, sG, L, D, u, gtab, part);
@@ -1038,6 +1038,22 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 #pragma unroll
                 for (int p = 0; p < P; p++) part[p] = SR::mul(gtab, SR::zero());
 #endif
+            };
+            int c = 0;
+            if constexpr (P == 1) {
+                // two cells per reduction: one permlane32 swap + DPP chain for both,
+                // and the two term sweeps are independent (overlapping latencies)
+                for (; c + 1 < nc; c += 2) {
+                    float pa[1], pb[1], ta, tb;
+                    cell_terms(c, pa);
+                    cell_terms(c + 1, pb);
+                    wave_sum2<SR>(pa[0], pb[0], ta, tb);
+                    sums[0] = (lane == c) ? ta : ((lane == c + 1) ? tb : sums[0]);
+                }
+            }
+            for (; c < nc; c++) {
+                float part[P], tot[P];
+                cell_terms(c, part);
                 wave_sums<SR, P>(part, tot);
 #pragma unroll
                 for (int p = 0; p < P; p++) sums[p] = (lane == c) ? tot[p] : sums[p];

@@ -5,5 +5,5 @@ export TMPDIR=/tmp
 rm -f gpurun_out/v/lat.txt
 for f in addapt_amd/_lib/ablate/lib_*.so; do
   ADX_LIB=$f timeout -k 10 120 python tools/pf_latency.py --fold mfe >> gpurun_out/v/lat.txt 2>&1
+  ADX_LIB=$f timeout -k 10 120 python tools/pf_latency.py --fold pf >> gpurun_out/v/lat.txt 2>&1
 done
-ADX_NO_MFE16=1 ADX_LIB=addapt_amd/_lib/ablate/lib_base.so timeout -k 10 120 python tools/pf_latency.py --fold mfe >> gpurun_out/v/lat.txt 2>&1
