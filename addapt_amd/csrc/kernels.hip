@@ -1383,7 +1383,11 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
         const int nc = N - d;
         const int od = off(d, N);
         const int umax = min(MAXLOOP_K, N - 3 - d);
-        for (int r = wid; r < nc; r += NW) {
+        // cells r = wid + k*NW of this wave: lane k keeps cell k's three sums and
+        // finishes it in the parallel tail below
+        float v_qmb = 0.f, v_rest = 0.f, v_int = 0.f;
+        int k = 0;
+        for (int r = wid; r < nc; r += NW, k++) {
             const int i = r + 1, j = i + d;
             const int idx = od + r;
             const bool pr = !SumProd::is_mark(L.qbm[0][idx]);
@@ -1425,25 +1429,21 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                         const int oidx = off(d + 2 + u, N) + a - 1;
                         const int ocd = O.oc[oidx];
                         const int t1 = (ocd * 41) >> 10;
-                        float f;
-                        if (k == TK_STK || k == TK_B1) {
-                            f = ct[CT_INVMM + ocd] * ct[CT_STK + t1 * 8 + ty2];
-                        } else if (k == TK_BUL) {
-                            f = ct[CT_BUL + ocd] * tau_in;
-                        } else if (k == TK_1N) {
-                            f = ct[CT_ONEN + ocd] * mo_in;
-                        } else if (k == TK_M23) {
-                            f = ct[CT_INVMM + ocd] * ct[CT_M23O + ocd] * m23_in;
-                        } else {   // 1x1, 1x2, 2x1, 2x2 tables (HBM / L2)
+                        // select form of the qb_terms factors (no divergent branches):
+                        // base (outer code) x second table factor x uniform inner factor
+                        const int base = (k == TK_BUL) ? CT_BUL : (k == TK_1N) ? CT_ONEN : CT_INVMM;
+                        const int sec = (k <= TK_B1) ? CT_STK + t1 * 8 + ty2 : (k == TK_M23) ? CT_M23O + ocd : CT_ONE;
+                        float um = (k == TK_BUL) ? tau_in : (k == TK_1N) ? mo_in : (k == TK_M23) ? m23_in : 1.f;
+                        if (k >= TK_I11 && k <= TK_I22) {   // 1x1, 1x2, 2x1, 2x2 tables (HBM / L2)
                             const int a1 = S[a + 1], b1 = S[b - 1], sp1 = S[i - 1], sq1 = S[j + 1];
-                            float tv;
-                            if (k == TK_I11) tv = T.int11[t1][ty2][a1][b1];
-                            else if (k == TK_I12) tv = T.int21[t1][ty2][a1][sq1][b1];
-                            else if (k == TK_I21) tv = T.int21[ty2][t1][sq1][a1][sp1];
-                            else tv = T.int22[t1][ty2][a1][sp1][sq1][b1];
-                            f = ct[CT_INVMM + ocd] * tv;
+                            const float *src;
+                            if (k == TK_I11) src = &T.int11[t1][ty2][a1][b1];
+                            else if (k == TK_I12) src = &T.int21[t1][ty2][a1][sq1][b1];
+                            else if (k == TK_I21) src = &T.int21[ty2][t1][sq1][a1][sp1];
+                            else src = &T.int22[t1][ty2][a1][sp1][sq1][b1];
+                            um = *src;
                         }
-                        sp = fmaf(O.qbb[oidx], f * sfv[s], sp);
+                        sp = fmaf(O.qbb[oidx], ct[base + ocd] * ct[sec] * (um * sfv[s]), sp);
                     }
                 }
                 a_int = fmaf(g, mmin, sp);
@@ -1451,32 +1451,39 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
             float s_qmb, s_rest;
             wave_sum2<SumProd>(a_qmb, a_rest, s_qmb, s_rest);
             const float s_int = wave_sum(a_int);
+            v_qmb = (lane == k) ? s_qmb : v_qmb;
+            v_rest = (lane == k) ? s_rest : v_rest;
+            v_int = (lane == k) ? s_int : v_int;
+        }
+        if (lane < k) {
+            const int r = wid + lane * NW;
+            const int i = r + 1, j = i + d;
+            const int idx = od + r;
+            const bool pr = !SumProd::is_mark(L.qbm[0][idx]);
             const float chain = (j < N && L.up[j + 1] >= 1) ? mlbase_sig * O.qm1b[((d + 1) & 1) * NP + i] : 0.f;
-            const float qm1b_v = s_qmb + s_rest + chain;
-            if (lane == 0) {
-                O.qmb[colb(j) + i - 1] = s_qmb;
-                O.Y[rowb(i, N) + d - 4] += s_qmb;     // X(i, j) was stored two diagonals ago
-                O.qm1b[(d & 1) * NP + i] = qm1b_v;
-                float qbbm = 0.f;
-                if (pr) {
-                    const int ty = ptype(S[i], S[j]);
-                    const float ext = L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
-                    const float stem = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
-                    const float qbb_v = s_int + O.q5b[j] * L.q5[0][i - 1] * ext + qm1b_v * stem;
-                    qbbm = qbb_v * L.dt[DT_MMI + O.oc[idx]];
-                    if (d - 2 >= 4)   // X(i+1, j-1): this pair closing a multiloop
-                        O.Y[rowb(i + 1, N) + d - 6] =
-                            qbb_v * mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
-                    const double qb = double(L.qbm[0][idx]) * double(ct[CT_INVMM + L.cc[idx]]);
-                    if (full) {
-                        const double pij = qb * double(qbb_v) / double(Z);
-                        full[size_t(i - 1) * ld + (j - 1)] = pij;
-                        full[size_t(j - 1) * ld + (i - 1)] = pij;
-                    }
-                    if (motif && d == mL - 1 && L.mat[i]) O.pm[i] = float(double(qbb_v) * XS->motif_extra / Z);
+            const float qm1b_v = v_qmb + v_rest + chain;
+            O.qmb[colb(j) + i - 1] = v_qmb;
+            O.Y[rowb(i, N) + d - 4] += v_qmb;     // X(i, j) was stored two diagonals ago
+            O.qm1b[(d & 1) * NP + i] = qm1b_v;
+            float qbbm = 0.f;
+            if (pr) {
+                const int ty = ptype(S[i], S[j]);
+                const float ext = L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
+                const float stem = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
+                const float qbb_v = v_int + O.q5b[j] * L.q5[0][i - 1] * ext + qm1b_v * stem;
+                qbbm = qbb_v * L.dt[DT_MMI + O.oc[idx]];
+                if (d - 2 >= 4)   // X(i+1, j-1): this pair closing a multiloop
+                    O.Y[rowb(i + 1, N) + d - 6] =
+                        qbb_v * mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
+                const double qb = double(L.qbm[0][idx]) * double(ct[CT_INVMM + L.cc[idx]]);
+                if (full) {
+                    const double pij = qb * double(qbb_v) / double(Z);
+                    full[size_t(i - 1) * ld + (j - 1)] = pij;
+                    full[size_t(j - 1) * ld + (i - 1)] = pij;
                 }
-                O.qbb[idx] = qbbm;
+                if (motif && d == mL - 1 && L.mat[i]) O.pm[i] = float(double(qbb_v) * XS->motif_extra / Z);
             }
+            O.qbb[idx] = qbbm;
         }
         __syncthreads();
     }
