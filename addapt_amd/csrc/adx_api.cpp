@@ -423,6 +423,12 @@ struct Problem {
     DevBuf<DevScaled> dX16;
     DevBuf<int> dOvf;
     bool mfe16 = false;
+    // incremental-fold state of the MC walkers (kernels.hip Inc)
+    DevBuf<float> dTab;
+    DevBuf<uint8_t> dCur, dValid;
+    DevBuf<int> dChg;
+    size_t tab_slot = 0;
+    bool state_on = false;   // set for MC launches only (not for adx_score_batch)
     std::unique_ptr<DevTables> hT;
     std::unique_ptr<DevScaled> hX;
 
@@ -474,6 +480,12 @@ struct Problem {
         ka.T16 = mfe16 ? dT16.p : nullptr;
         ka.X16 = mfe16 ? dX16.p : nullptr;
         ka.ovf = mfe16 ? dOvf.p : nullptr;
+        const bool st = state_on && dTab.p && !std::getenv("ADX_NO_INCR");
+        ka.tab = st ? dTab.p : nullptr;
+        ka.tab_slot = tab_slot;
+        ka.cur_slot = st ? dCur.p : nullptr;
+        ka.tab_valid = st ? dValid.p : nullptr;
+        ka.chg = st ? dChg.p : nullptr;
         return ka;
     }
 
@@ -526,6 +538,19 @@ struct Problem {
         HIP_TRY(dX16.upload(X16.get(), 1, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         mfe16 = true;
+        return ADX_OK;
+    }
+    // per walker two slots of every group's tables: sized for the largest kernel
+    // configuration (P = 2 value arrays, one group per variant)
+    adx_status alloc_state(int W) {
+        tab_slot = size_t(variants.size()) * inc_group_floats(kargs().cells, Nmax, 2);
+        HIP_TRY(dTab.alloc(size_t(W) * 2 * tab_slot));
+        HIP_TRY(dCur.alloc(W));
+        HIP_TRY(dValid.alloc(W));
+        HIP_TRY(dChg.alloc(size_t(W) * 2));
+        HIP_TRY(hipMemsetAsync(dCur.p, 1, W, stream));     // the initial fold writes slot 0
+        HIP_TRY(hipMemsetAsync(dValid.p, 0, W, stream));
+        HIP_TRY(hipMemsetAsync(dChg.p, 0xff, sizeof(int) * 2 * W, stream));
         return ADX_OK;
     }
     adx_status ensure_ovf(int W) {
@@ -1122,9 +1147,15 @@ extern "C" adx_status adx_walkers_init(adx_ctx *c, int W, const char *seqs, cons
     HIP_TRY(hipMemsetAsync(c->err.p, 0, sizeof(int) * W, pb.stream));
     std::vector<double> t0(W, c->thermo.t_init);
     HIP_TRY(hipMemcpyAsync(c->auto_T.p, t0.data(), sizeof(double) * W, hipMemcpyHostToDevice, pb.stream));
-    // initial score (sampling.cc:40)
-    adx_status s = pb.score(c->cur_seq.p, W, c->cur_score.p, nullptr, nullptr);
+    // initial score (sampling.cc:40); it also stores the walkers' first tables
+    adx_status s = pb.alloc_state(W);
     if (s) return s;
+    pb.state_on = true;
+    s = pb.score(c->cur_seq.p, W, c->cur_score.p, nullptr, nullptr);
+    pb.state_on = false;
+    if (s) return s;
+    HIP_TRY(hipMemsetAsync(pb.dCur.p, 0, W, pb.stream));
+    HIP_TRY(hipMemsetAsync(pb.dValid.p, 1, W, pb.stream));
     HIP_TRY(hipStreamSynchronize(pb.stream));
     return ADX_OK;
 }
@@ -1148,6 +1179,7 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     st.prop_seq = c->prop_seq.p;
     st.prop_score = c->prop_score.p;
     st.changed = c->changed.p;
+    st.chg = c->pb.dChg.p;
     st.pick = c->pick.p;
     st.bcode = c->bcode.p;
     st.temp = c->temp.p;
@@ -1201,7 +1233,10 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
         ~EvFree() { for (auto e : v) (void)hipEventDestroy(e); }
     } evfree{evs};
     HIP_TRY(hipEventRecord(c->ev0, pb.stream));
-    HIP_TRY(launch_steps(pb.kargs(), pb.qbm, st, pb.stream, evs.data()));
+    pb.state_on = true;   // incremental folds against the walkers' stored tables
+    const KArgs ka_steps = pb.kargs();
+    pb.state_on = false;
+    HIP_TRY(launch_steps(ka_steps, pb.qbm, st, pb.stream, evs.data()));
     HIP_TRY(hipEventRecord(c->ev1, pb.stream));
     HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0.f;
@@ -1291,6 +1326,8 @@ extern "C" adx_status adx_walkers_import(adx_ctx *c, const void *dev_seqs, const
     if (dev_seqs) HIP_TRY(hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
     if (dev_scores)
         HIP_TRY(hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_seqs && c->pb.dValid.p)   // new configurations: their next fold starts from scratch
+        HIP_TRY(hipMemsetAsync(c->pb.dValid.p, 0, W, c->pb.stream));
     HIP_TRY(hipStreamSynchronize(c->pb.stream));
     return ADX_OK;
 }

@@ -123,6 +123,12 @@ __host__ __device__ inline uint32_t hp_key(const uint8_t *S, int i, int len) {
     return k;
 }
 
+// floats of one fold group's tables in the incremental-fold state: per value
+// array qbm, qm, qm1 (cells each) and q5 (Nmax + 2)
+__host__ __device__ inline size_t inc_group_floats(int cells, int Nmax, int P) {
+    return size_t(P) * (3 * size_t(cells) + size_t(Nmax) + 2);
+}
+
 struct KArgs {
     const DevTables *T;
     const DevScaled *X;
@@ -153,6 +159,14 @@ struct KArgs {
     const DevTables *T16;
     const DevScaled *X16;
     int *ovf;
+    // incremental folds (kernels.hip Inc): per walker two slots of every group's
+    // tables (tab_slot floats each), the current slot and whether it is valid,
+    // and the hull of the positions the step's proposal changed (-1: none)
+    float *tab;
+    size_t tab_slot;
+    uint8_t *cur_slot;
+    uint8_t *tab_valid;
+    const int *chg;
 };
 
 // Monte Carlo state (device, read/write).
@@ -192,6 +206,7 @@ struct StepArgs {
     int32_t *tr_outcome;
     double *tr_temp, *tr_prop, *tr_cur, *tr_u;
     double *tr_terms;           // [(s*W + w) * n_terms_total]
+    int *chg;                   // W * 2: hull of the positions the proposal changed (-1: none)
 };
 
 }  // namespace adx

@@ -497,11 +497,11 @@ struct RangeCost {
 };
 
 template <int P>
-__host__ __device__ inline RangeCost range_cost(int d, int N, int cp) {
+__host__ __device__ inline RangeCost range_cost(int d, int N, int cp, int cq) {
     RangeCost r;
     const int sq = d - 1;                                   // qm span
     r.cp = cp;
-    r.cq = (sq >= 4 && sq <= N - 3) ? N - sq : 0;
+    r.cq = cq;                                              // qm cells of span sq to fold
     r.umax = d - 6 < 30 ? d - 6 : 30;
     // |S|, |G| of the terms with u <= umax (dev_types.hpp lists, closed form)
     r.nS = r.umax < 0 ? 0 : r.umax <= 5 ? ((r.umax + 1) * (r.umax + 2)) / 2 : 21 + 4 * (r.umax - 5);
@@ -555,9 +555,24 @@ __device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
 // split sum mla(i+1, j-1) that the qm item of the previous iteration kept.  A qm
 // item is 4 cells x 16 lanes (split points).  Items are cut into NW contiguous
 // ranges of equal estimated cost, one per wave.
+// Incremental folds.  An MC proposal differs from the walker's current
+// sequence at a few positions; a cell (i,j) depends on S[i-1..j+1] only, so
+// every cell whose [i-1, j+1] misses the changed positions keeps its value.
+// src: the group's tables of the current sequence (HBM, null = fold all);
+// dst: where this fold's tables go (null = nowhere); [m_lo, m_hi]: the hull of
+// the changed positions, 1-based folded coordinates.  Per diagonal d the
+// changed cells are i in [max(1, m_lo-1-d), min(N-d, m_hi+1)]; the qm items
+// take one cell more on each side (the multiloop-closing sums of changed
+// pairs), q5[j] is recomputed from j = m_lo-1 on.
+struct Inc {
+    const float *src;
+    float *dst;
+    int m_lo, m_hi;
+};
+
 template <int NT, int P, class SR>
 __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, const Lds<P> &L,
-                         const DevScaled *__restrict__ XS, float (&z)[P], bool &bad) {
+                         const DevScaled *__restrict__ XS, float (&z)[P], bool &bad, const Inc &inc) {
     constexpr int NW = NT / WAVE;
     const DevVariant V = ka.variants[vs[0]];
     // motif[p]: table p carries a holo variant; NV = 2 packs variants vs[2p], vs[2p+1]
@@ -578,6 +593,18 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     const int lane = tid & (WAVE - 1);
     const int wid = uni(tid / WAVE);
     const int NP = L.np;
+    // incremental fold (Inc): changed cells of diagonal dd are i in [clo, chi],
+    // qm items of span s are i in [qlo, qhi]
+    const bool incr = inc.src != nullptr;
+    const int m_lo = uni(inc.m_lo), m_hi = uni(inc.m_hi);
+    auto clo = [&](int dd) { return incr ? max(1, m_lo - 1 - dd) : 1; };
+    auto chi = [&](int dd) { return incr ? min(N - dd, m_hi + 1) : N - dd; };
+    auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
+    auto qcount = [&](int sq) {
+        if (sq < 4 || sq > N - 3) return 0;
+        const int hi = incr ? min(N - sq, m_hi + 2) : N - sq;
+        return max(0, hi - qlo(sq) + 1);
+    };
 
     // ---- per-group setup: sequence, constraint arrays, motif sites
     const uint8_t *cons = ka.cons + V.cons_off;
@@ -698,9 +725,9 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 }
                 L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
             }
-            base += __popcll(__ballot(pr));
+            base += __popcll(__ballot(pr && r + 1 >= clo(dd) && r + 1 <= chi(dd)));
         }
-        if (lane == 0) L.pcnt[dd] = static_cast<uint8_t>(base);
+        if (lane == 0) L.pcnt[dd] = static_cast<uint8_t>(base);   // pairable cells to fold
     }
     __syncthreads();
     const bool has_rec = L.rec || L.rec32;
@@ -728,7 +755,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             int base = 0;
             for (int r0 = 0; r0 < c; r0 += WAVE) {
                 const int r = r0 + lane;
-                const bool pr = r < c && !SR::is_mark(L.qbm[0][od + r]);
+                const bool pr = r < c && !SR::is_mark(L.qbm[0][od + r]) && r + 1 >= clo(dd) && r + 1 <= chi(dd);
                 const unsigned long long bm = __ballot(pr);
                 if (pr) {
                     const int k = rb + base + __popcll(bm & ((1ull << lane) - 1ull));
@@ -749,13 +776,37 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     if (L.rt) {
         for (int t = tid; t < (N - 3) * NW; t += NT) {
             const int d = 4 + t / NW, w = t % NW;
-            RangeCost rc = range_cost<P>(d, N, d <= N - 1 ? int(L.pcnt[d]) : 0);
+            RangeCost rc = range_cost<P>(d, N, d <= N - 1 ? int(L.pcnt[d]) : 0, qcount(d - 1));
             int r[4];
             wave_range<NW>(rc, w, r);
             L.rt[d * NW + w] = uint32_t(r[0]) | (uint32_t(r[1]) << 8) | (uint32_t(r[2]) << 16) | (uint32_t(r[3]) << 24);
         }
     }
     if (L.rt || has_rec) __syncthreads();
+
+    // ---------------- incremental fold: the unchanged cells from the previous tables
+    if (incr) {
+        const size_t C = size_t(ka.cells);
+        for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
+            const int lo = clo(dd), hi = chi(dd), od = off(dd, N);
+            for (int r = lane; r < N - dd; r += WAVE) {
+                const int i = r + 1, j = i + dd;
+                if (i >= lo && i <= hi) continue;
+#pragma unroll
+                for (int p = 0; p < P; p++) {
+                    const float *sp = inc.src + p * (3 * C + NP);
+                    L.qbm[p][od + r] = sp[od + r];
+                    L.qm[p][rowb(i, N) + dd - 4] = sp[C + rowb(i, N) + dd - 4];
+                    L.qm1[p][colb(j) + i - 1] = sp[2 * C + colb(j) + i - 1];
+                }
+            }
+        }
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) {
+#pragma unroll
+            for (int p = 0; p < P; p++) L.q5[p][k] = inc.src[p * (3 * C + NP) + 3 * C + k];
+        }
+        __syncthreads();
+    }
 
     // ---------------- loop-carried state.  prep(d) runs at the end of
     // iteration d-1 (before its barrier) and fills everything iteration d needs
@@ -823,7 +874,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             int base = 0;
             for (int r0 = 0; r0 < N - d && base < kc + nc; r0 += WAVE) {
                 const int r = r0 + lane;
-                const bool pr = r < N - d && !SR::is_mark(L.qbm[0][od + r]);
+                const bool pr = r < N - d && !SR::is_mark(L.qbm[0][od + r]) && r + 1 >= clo(d) && r + 1 <= chi(d);
                 const unsigned long long m = __ballot(pr);
                 const int rank = base + __popcll(m & ((1ull << lane) - 1ull));
                 if (pr && rank >= kc && rank < kc + nc) ws[rank - kc] = static_cast<uint8_t>(r + 1);
@@ -876,7 +927,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
     };
 
     auto prep = [&](int d) {
-        const RangeCost rc = range_cost<P>(d, N, uni((d <= N - 1) ? L.pcnt[d] : 0));
+        const RangeCost rc = range_cost<P>(d, N, uni((d <= N - 1) ? L.pcnt[d] : 0), qcount(d - 1));
         cp = rc.cp;
         cq = rc.cq;
         umax = rc.umax;
@@ -966,10 +1017,11 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         {
             const int g = lane >> 4, l16 = lane & 15;
             const int tmax = sq - 4;
+            const int q0 = qlo(sq);   // first qm cell of this iteration's items
             for (int m0 = km_lo; m0 < km_hi; m0 += 4) {
                 const int m = m0 + g;
                 const bool cell = m < km_hi;
-                const int i = m + 1, jb = i + sq;
+                const int i = q0 + m, jb = i + sq;
                 const int upi = constrained ? L.up[cell ? i : 1] : 255;
                 const int o1 = colb(jb) + i - 1, orr = rowb(i, N) - 5;
                 float A[P], Pp[P];
@@ -1071,7 +1123,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 
         // ---------------- q5[d] (the last wave: q5 is last in the cost order)
 #ifndef ADX_ABL_Q5
-        if (wid == NW - 1) {
+        if (wid == NW - 1 && (!incr || d >= m_lo - 1)) {   // q5[j < m_lo - 1] is unchanged
 #else
         if (false) {
 #endif
@@ -1101,7 +1153,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             }
         }
         STAMP(6);
-        if (has1 && m1np) {
+        if (has1 && m1np && i1 >= clo(d) && i1 <= chi(d)) {
 #pragma unroll
             for (int p = 0; p < P; p++)
                 L.qm1[p][colb(j1) + i1 - 1] = (d >= 5 && m1up >= 1) ? SR::mul(m1prev[p], mlbase_sig) : SR::zero();
@@ -1117,6 +1169,19 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
 #endif
 #pragma unroll
     for (int p = 0; p < P; p++) z[p] = L.q5[p][N];   // scaled Z; energies after the group loop
+    if (inc.dst) {   // this fold's tables: the next proposal's unchanged cells
+        const size_t C = size_t(ka.cells);
+#pragma unroll
+        for (int p = 0; p < P; p++) {
+            float *dp = inc.dst + p * (3 * C + NP);
+            for (int k = tid; k < int(C); k += NT) {
+                dp[k] = L.qbm[p][k];
+                dp[C + k] = L.qm[p][k];
+                dp[2 * C + k] = L.qm1[p][k];
+            }
+            for (int k = tid; k <= N; k += NT) dp[3 * C + k] = L.q5[p][k];
+        }
+    }
     bad = false;
     if constexpr (SR::NV == 2) {
         // exactness guard of the 16-bit encoding (MinPlus16): every stored value >= floor
@@ -1166,7 +1231,7 @@ __device__ double combine_score(const KArgs &ka, const Lds<P> &L, const double *
 template <int NT, int P, class SR>
 __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ XS,
                                  const uint8_t *raw, const Lds<P> &L, const double *pp,
-                                 float *dG_out, double *terms_out, bool &any_bad) {
+                                 float *dG_out, double *terms_out, bool &any_bad, int w) {
     const int ng = P * SR::NV == 2 ? ka.n_groups2 : ka.n_variants;
     any_bad = false;
     for (int g = 0; g < ng; g++) {
@@ -1179,7 +1244,20 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
         }
         float z[P];
         bool bad = false;
-        pf_group<NT, P, SR>(ka, vs, raw, L, XS, z, bad);
+        Inc inc{nullptr, nullptr, 0, 0};
+        if (ka.tab) {   // MC state: read the current tables, write this proposal's
+            const size_t G = inc_group_floats(ka.cells, ka.Nmax, P);
+            const int cur = ka.cur_slot[w];
+            float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
+            inc.dst = base + size_t(1 - cur) * ka.tab_slot + size_t(g) * G;
+            if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+                const int lb = ka.variants[vs[0]].before_len;
+                inc.src = base + size_t(cur) * ka.tab_slot + size_t(g) * G;
+                inc.m_lo = ka.chg[2 * w] + 1 + lb;
+                inc.m_hi = ka.chg[2 * w + 1] + 1 + lb;
+            }
+        }
+        pf_group<NT, P, SR>(ka, vs, raw, L, XS, z, bad, inc);
         any_bad |= bad;
         if (threadIdx.x == 0) {
             if constexpr (SR::NV == 2) {
@@ -1228,10 +1306,13 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
     bool bad = false;
     const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, pp, dG ? dG + size_t(w) * ka.n_variants : nullptr,
-                                          terms ? terms + size_t(w) * nt : nullptr, bad);
+                                          terms ? terms + size_t(w) * nt : nullptr, bad, w);
     if (threadIdx.x == 0) {
         scores[w] = s;
-        if (SR::NV == 2 && bad && ka.ovf) ka.ovf[w] = 1;   // re-folded by the FP32 MinPlus kernel
+        if (SR::NV == 2 && bad && ka.ovf) {
+            ka.ovf[w] = 1;                         // re-folded by the FP32 MinPlus kernel
+            if (ka.tab) ka.tab_valid[w] = 0;       // and folded from scratch next time
+        }
     }
 }
 
@@ -1548,7 +1629,7 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
     const int vs[1] = {v};
     float z[1];
     bool bad = false;
-    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z, bad);
+    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z, bad, Inc{nullptr, nullptr, 0, 0});
     __syncthreads();
     outside<NT>(ka, v, bv, L, O, XS, z[0],
                 full ? full + (size_t(w) * ka.n_bvars + bv) * size_t(ld) * ld : nullptr, ld,
@@ -1691,13 +1772,23 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
     const int bcode = int(mt_uniform(a, 4u, lane)) + 1;  // "ACGU"[r]
     const int e = st.clo_err[pick];
     bool changed = false;
+    int plo = 1 << 30, phi = -1;   // hull of the positions whose base changes (incremental folds)
     if (e == 0) {
         for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE) {
             const int pos = st.clo_pos[k];
             const int nb = st.clo_par[k] ? 5 - bcode : bcode;
-            if (cur[pos] != nb) changed = true;
+            if (cur[pos] != nb) {
+                changed = true;
+                plo = min(plo, pos);
+                phi = max(phi, pos);
+            }
         }
         changed = __ballot(changed) != 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            plo = min(plo, __shfl_xor(plo, o, WAVE));
+            phi = max(phi, __shfl_xor(phi, o, WAVE));
+        }
     }
     double u = 0.0;
     if (e == 0 && changed) u = mt_canonical(c, lane);
@@ -1720,6 +1811,10 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
         st.temp[w] = T;
         st.u[w] = u;
         st.changed[w] = (e != 0) ? 0 : (changed ? 1 : 0);
+        if (st.chg) {
+            st.chg[2 * w] = changed ? plo : -1;
+            st.chg[2 * w + 1] = changed ? phi : -1;
+        }
         if (e != 0) st.err[w] = e;
         if (st.tr_pos) {
             const size_t r = size_t(s) * st.W + w;
@@ -1730,7 +1825,7 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
     }
 }
 
-__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot) {
+__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot, uint8_t *cur_slot) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= st.W || st.err[w]) return;
     const bool changed = st.changed[w] == 1;
@@ -1745,6 +1840,7 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
         } else {
             outcome = (diff > 0) ? 3 : 1;
             st.cur_score[w] = prop;
+            if (cur_slot) cur_slot[w] ^= 1;   // the proposal's tables become current
             const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
             uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
             for (int k = 0; k < st.Nraw; k++) c[k] = p[k];
@@ -1846,9 +1942,11 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         k16.X = ka.X16;
         hipError_t e = launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         if (e != hipSuccess) return e;
+        KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state
+        kf.tab = nullptr;
         if (choose_p(ka) == 2)
-            return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, ka.ovf, stream);
-        return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, ka.ovf, stream);
+            return launch_score_t<ADX_NT2, 2, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
+        return launch_score_t<512, 1, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
     }
     if (ka.mode == 1) {
         if (choose_p(ka) == 2)
@@ -1924,7 +2022,8 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot);
+        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,
+                           ka.tab ? ka.cur_slot : nullptr);
     }
     return hipGetLastError();
 }
