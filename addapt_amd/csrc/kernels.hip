@@ -48,6 +48,16 @@ __device__ __forceinline__ int off(int dd, int N) { return ((dd - 4) * (2 * N - 
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Workgroup barrier ordering LDS only (the fold's waves share nothing else
+// inside its diagonal loop): outstanding global loads are not drained, so a
+// prefetch issued before the barrier completes in the shadow of the next
+// iteration instead of stalling the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ---------------------------------------------------------------- semirings
 // One kernel body folds both energy models:
 //   SumProd  McCaskill partition function: FP32 Boltzmann factors with the pf
@@ -1160,7 +1170,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         }
         if (d < N) prep(d + 1);
         STAMP(7);
-        __syncthreads();
+        lds_barrier();   // LDS only: the table prefetch of prep(d+1) stays in flight
         STAMP(9);
     }
 #ifdef ADX_STAMP
