@@ -209,3 +209,57 @@ def test_mc_mfe_full_size_invariants(native, oracle):
     for w in list(range(0, W, 257)) + [W - 1]:
         ref, _ = sf.score(final[w], [active])
         assert _close(scores[w], ref), (w, scores[w], ref)
+
+
+@pytest.mark.parametrize("fold", ["mfe", "pf"])
+def test_mc_trajectory_contexts_incremental(native, oracle, fold):
+    """Contexts shift the changed positions of every fold by the context's
+    prefix: incremental refolds must match the oracle's full folds step by step."""
+    tmpl, active = workloads.synthetic(60)
+    terms = workloads.default_objective()
+    ctx = [("GGAC", "UUA"), ("", "CCCA"), ("AUAUAU", "")]
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt, contexts=ctx, fold_mode=fold, thermostat=th)
+    seeds = [3, 4, 5, 6]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    steps = 30
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    sf = oracle.ScoreFunction(terms, aptamer=m, contexts=ctx, mode=fold)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    tie = 1e-12 if fold == "mfe" else 1e-6
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=tie)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                a, b = tr["proposed_score"][s, w], ref["proposed_score"][s]
+                if fold == "mfe":
+                    assert _close(a, b), (w, s, a, b)
+                else:
+                    assert a == b or abs(a - b) <= 2e-3, (w, s, a, b)
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert list(counters[w]) == ref["counters"]
+
+
+def test_mc_mfe_full_size_incremental_consistency(native, oracle):
+    """After many incremental steps at config-2 size, every walker's score equals
+    a from-scratch score of its final sequence (adx_score_batch, no state)."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    W = 1024
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(40)
+    final, scores, counters = eng.download()
+    sc, _, _ = eng.score_batch(final)
+    for w in range(W):
+        assert _close(scores[w], sc[w]), (w, scores[w], sc[w])

@@ -206,3 +206,20 @@ def test_mc_large_batch_invariants(native, oracle):
             assert s[len(s) - 1 - k] == comp[s[k]]
         ref, _ = sf.score(s, [active])
         assert abs(scores[w] - ref) <= 2e-3
+
+
+def test_mc_pf_incremental_consistency(native, oracle):
+    """Incremental refolds (stored tables + changed cells) give the scores a
+    from-scratch fold gives: 1024 walkers x 40 steps, then adx_score_batch."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    W = 1024
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(40)
+    final, scores, counters = eng.download()
+    sc, _, _ = eng.score_batch(final)
+    for w in range(W):
+        assert scores[w] == sc[w] or abs(scores[w] - sc[w]) <= 1e-6 * max(1.0, abs(sc[w])), (w, scores[w], sc[w])
