@@ -161,6 +161,11 @@ def main():
         flop_per_scored += 2 * (f_free + f_out)
     launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
     achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
+    # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
+    # groups x value arrays (MFE: one packed apo/holo array; PF: two) x
+    # (3 cell tables + q5) x 4 B
+    cells = (a.length - 4) * (a.length - 3) // 2
+    state_bytes = 2 * (1 if a.fold == "mfe" else 2) * (3 * cells + a.length + 2) * 4
     traffic, traffic_src = None, None
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", "traffic_latest_%s.json" % a.fold)
@@ -189,9 +194,11 @@ def main():
         "flop_per_scored_step": flop_per_scored,
         "flop_per_launch": launch_flops,
         "scored_walkers_per_launch": scored / max(1, a.steps),
-        # compulsory HBM bytes of one launch: each scored walker reads its
-        # proposal (N B) and writes its score (8 B)
-        "algorithmic_bytes_per_launch": (scored / max(1, a.steps)) * (a.length + 8),
+        # HBM bytes of one launch by design: each scored walker reads its proposal
+        # (N B), writes its score (8 B), and writes its fold tables for the next
+        # incremental refold (read back for the unchanged cells, <= the same again)
+        "algorithmic_bytes_per_launch": (scored / max(1, a.steps)) * (a.length + 8 + 2 * state_bytes),
+        "state_bytes_per_scored_walker": state_bytes,
     }
     out = {
         "metric": METRIC,
