@@ -238,6 +238,10 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
             X.fgen[(u - 6) * FG_ROW + n1 - 2] =
                 n2 >= 2 ? F(P.interior[u] + std::min(P.maxninio, std::abs(n1 - n2) * P.ninio), u + 2) : F.zero();
         }
+    for (int k = 0; k < 32; k++) {
+        X.il[k] = (mfe && k <= MAXLOOP) ? static_cast<float>(P.interior[k]) : 0.f;
+        X.nin[k] = mfe ? static_cast<float>(std::min(P.maxninio, k * P.ninio)) : 0.f;
+    }
     // term lists ordered by u (dev_types.hpp NS_MAX)
     int ns = 0, ng = 0;
     auto addS = [&](int kind, int n1, int n2, float f) {
@@ -529,7 +533,7 @@ struct Problem {
         auto T16 = std::make_unique<DevTables>(*hT);
         auto X16 = std::make_unique<DevScaled>(*hX);
         bool ok = pack16(reinterpret_cast<float *>(T16.get()), sizeof(DevTables) / sizeof(float));
-        ok = ok && pack16(X16->ctab, CT_SIZE) && pack16(X16->fgen, FG_SIZE) && pack16(X16->s_f, NS_MAX) &&
+        ok = ok && pack16(X16->ctab, CT_SIZE) && pack16(X16->fgen, FG_SIZE) && pack16(X16->il, 32) && pack16(X16->nin, 32) && pack16(X16->s_f, NS_MAX) &&
              pack16(X16->g_f, NG_MAX) && pack16(X16->sig, NMAX + 4) && pack16(X16->hp, NMAX + 1) &&
              pack16(X16->pwml, NMAX + 1) && pack16(&X16->mlclosing, 1) && pack16(&X16->mlbase_sig, 1) &&
              pack16(X16->sp_val, MAX_SPECIAL_HP) && pack16(&X16->motif_extra, 1);

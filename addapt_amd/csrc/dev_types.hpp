@@ -76,6 +76,9 @@ struct DevTables {         // exp(-E/kT) (PF) or E (MFE), FP32; pair type 0 rows
 struct DevScaled {
     float ctab[CT_SIZE];     // see CT_* (copied to LDS)
     float fgen[FG_SIZE];     // generic interior factors
+    // MFE only (mfe_cells.hip): generic interior energy = il[u] + nin[|n1 - n2|]
+    float il[32];            // interior[u]
+    float nin[32];           // min(MAX_NINIO, k * ninio)
     // interior term lists (see NS_MAX); *_cnt[umax] = terms with u <= umax
     uint8_t s_n1[NS_MAX], s_n2[NS_MAX], s_kind[NS_MAX];
     float s_f[NS_MAX];       // constant factor (sigma power, bulge / 1xn length)

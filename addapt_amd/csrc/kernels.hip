@@ -25,8 +25,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "dev_types.hpp"
+#include "fold_common.hpp"
 
 namespace adx {
 
@@ -41,22 +44,6 @@ __device__ unsigned long long g_stamps[16][16];
 
 namespace {
 
-constexpr int WAVE = 64;
-
-// index of the first cell of diagonal dd (cells with j - i = dd >= 4)
-__device__ __forceinline__ int off(int dd, int N) { return ((dd - 4) * (2 * N - 3 - dd)) >> 1; }
-
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-
-// Workgroup barrier ordering LDS only (the fold's waves share nothing else
-// inside its diagonal loop): outstanding global loads are not drained, so a
-// prefetch issued before the barrier completes in the shadow of the next
-// iteration instead of stalling the barrier.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 // ---------------------------------------------------------------- semirings
 // One kernel body folds both energy models:
@@ -102,8 +89,6 @@ struct MinPlus {
 // is reset to 0x7FFF when a cell is stored (fin).  Exact while every stored
 // value stays >= MFE16_FLOOR (checked at the end of the fold; a walker that
 // fails the check is re-folded by the FP32 MinPlus kernel).
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-constexpr int MFE16_FLOOR = -12000;
 struct MinPlus16 {
     static constexpr bool MFE = true;
     static constexpr int NV = 2;
@@ -172,40 +157,7 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-// Pair type / reversed type / terminal-AU flag without a memory lookup:
-// PAIR[a][b] for codes a, b in 0..4 (ViennaRNA types 1..6) packed 3 bits per
-// entry of index 5a+b-9 (the canonical pairs sit at 9..23).
-constexpr unsigned long long pack_pairs() {
-    unsigned long long k = 0;
-    k |= 5ull << (3 * (9 - 9));    // A-U
-    k |= 1ull << (3 * (13 - 9));   // C-G
-    k |= 2ull << (3 * (17 - 9));   // G-C
-    k |= 3ull << (3 * (19 - 9));   // G-U
-    k |= 6ull << (3 * (21 - 9));   // U-A
-    k |= 4ull << (3 * (23 - 9));   // U-G
-    return k;
-}
-__device__ __forceinline__ int ptype(int a, int b) {
-    const int idx = 5 * a + b - 9;
-    return (idx >= 0 && idx <= 14) ? int((pack_pairs() >> (3 * idx)) & 7ull) : 0;
-}
-__device__ __forceinline__ int rtype(int t) { return t ? (((t - 1) ^ 1) + 1) : 0; }
 
-// Cell indexing (1-based i < j, span j - i >= 4):
-//   qbm, cc  diagonal-major  off(j-i) + i - 1   (cells of one anti-diagonal contiguous)
-//   qm       row-major       rowb(i) + j - i - 4 (qm[i][*] contiguous)
-//   qm1      column-major    colb(j) + i - 1     (qm1[*][j] contiguous)
-// so every inner loop of the recurrence walks contiguous LDS at a per-lane base.
-__device__ __forceinline__ int rowb(int i, int N) { return (i - 1) * (N - 3) - (((i - 1) * i) >> 1); }
-__device__ __forceinline__ int colb(int j) { return ((j - 5) * (j - 4)) >> 1; }
-
-// LDS per-cell table block (L.dt), copied from DevTables / DevScaled
-constexpr int DT_MMH = 0;      // [type][x][y] hairpin mismatch
-constexpr int DT_MMI = 200;    // [type][x][y] interior mismatch
-constexpr int DT_MLS = 400;    // [type][x][y] multiloop stem
-constexpr int DT_EXT = 600;    // [type][6][6] exterior stem
-constexpr int DT_TAU = 888;    // [type] terminal AU
-constexpr int DT_HP = 896;     // [u] hairpin length factor
 
 constexpr int CHUNK = 16;      // closing-pair cells per chunk of one wave (4 prefetch lanes each)
 constexpr int GSLOTS = NG_MAX / WAVE;   // 6
@@ -1941,6 +1893,19 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
     return hipGetLastError();
 }
 
+size_t mfe_cells_lds(const KArgs &ka);
+hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
+                            const int *mask, hipStream_t stream);
+
+// ADX_MFE_KERNEL=cells moves the MFE to mfe_cells_kernel (lanes = cells)
+static bool use_mfe_cells() {
+    static const int v = [] {
+        const char *e = std::getenv("ADX_MFE_KERNEL");
+        return (e && std::strcmp(e, "cells") == 0) ? 1 : 0;
+    }();
+    return v != 0;
+}
+
 hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
                           float *dG, const int *mask, hipStream_t stream) {
     // ka.mode: 0 = partition functions (vrna_pf), 1 = minimum free energies
@@ -1950,7 +1915,9 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         KArgs k16 = ka;
         k16.T = ka.T16;
         k16.X = ka.X16;
-        hipError_t e = launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
+        hipError_t e = (use_mfe_cells() && mfe_cells_lds(k16) > 0)
+                           ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
+                           : launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         if (e != hipSuccess) return e;
         KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state
         kf.tab = nullptr;
