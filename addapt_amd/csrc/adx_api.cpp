@@ -427,6 +427,7 @@ struct Problem {
     DevBuf<DevScaled> dX16;
     DevBuf<int> dOvf;
     bool mfe16 = false;
+    bool mfe_cells_ok = false;   // Ninio saturated from |n1-n2| = 5 on, MLbase >= 0 (mfe_cells.hip)
     // incremental-fold state of the MC walkers (kernels.hip Inc)
     DevBuf<float> dTab;
     DevBuf<uint8_t> dCur, dValid;
@@ -484,6 +485,7 @@ struct Problem {
         ka.T16 = mfe16 ? dT16.p : nullptr;
         ka.X16 = mfe16 ? dX16.p : nullptr;
         ka.ovf = mfe16 ? dOvf.p : nullptr;
+        ka.mfe_cells_ok = mfe16 && mfe_cells_ok ? 1 : 0;
         const bool st = state_on && dTab.p && !std::getenv("ADX_NO_INCR");
         ka.tab = st ? dTab.p : nullptr;
         ka.tab_slot = tab_slot;
@@ -542,6 +544,9 @@ struct Problem {
         HIP_TRY(dX16.upload(X16.get(), 1, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         mfe16 = true;
+        mfe_cells_ok = P->MLbase >= 0;
+        for (int k = 5; k <= MAXLOOP; k++)
+            if (std::min(P->maxninio, k * P->ninio) != std::min(P->maxninio, 5 * P->ninio)) mfe_cells_ok = false;
         return ADX_OK;
     }
     // per walker two slots of every group's tables: sized for the largest kernel

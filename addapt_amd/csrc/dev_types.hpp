@@ -162,6 +162,7 @@ struct KArgs {
     const DevTables *T16;
     const DevScaled *X16;
     int *ovf;
+    int mfe_cells_ok;           // the lanes = cells MFE kernel covers this energy model (mfe_cells.hip)
     // incremental folds (kernels.hip Inc): per walker two slots of every group's
     // tables (tab_slot floats each), the current slot and whether it is valid,
     // and the hull of the positions the step's proposal changed (-1: none)
