@@ -1897,13 +1897,21 @@ size_t mfe_cells_lds(const KArgs &ka);
 hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
                             const int *mask, hipStream_t stream);
 
-// ADX_MFE_KERNEL=cells moves the MFE to mfe_cells_kernel (lanes = cells)
-static bool use_mfe_cells() {
+size_t mfe_quad_lds(const KArgs &ka);
+hipError_t launch_mfe_quad(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
+                           const int *mask, hipStream_t stream);
+
+// MFE kernel choice, ADX_MFE_KERNEL: rows = score_kernel<MinPlus16> (lanes = terms),
+// cells = mfe_cells_kernel (lanes = cells, two folds per cell), quad = mfe_quad_kernel
+// (lanes = cells, four folds per cell)
+static int mfe_kernel_choice() {
     static const int v = [] {
         const char *e = std::getenv("ADX_MFE_KERNEL");
-        return (e && std::strcmp(e, "cells") == 0) ? 1 : 0;
+        if (e && std::strcmp(e, "cells") == 0) return 1;
+        if (e && std::strcmp(e, "quad") == 0) return 2;
+        return 0;
     }();
-    return v != 0;
+    return v;
 }
 
 hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
@@ -1915,8 +1923,9 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         KArgs k16 = ka;
         k16.T = ka.T16;
         k16.X = ka.X16;
-        hipError_t e = (use_mfe_cells() && mfe_cells_lds(k16) > 0)
-                           ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
+        const int kc = mfe_kernel_choice();
+        hipError_t e = (kc == 2 && mfe_quad_lds(k16) > 0)    ? launch_mfe_quad(k16, seqs, W, scores, terms, dG, mask, stream)
+                       : (kc >= 1 && mfe_cells_lds(k16) > 0) ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
                            : launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         if (e != hipSuccess) return e;
         KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state

@@ -68,6 +68,202 @@ def partition():
     return [sorted(b) for b in blocks], load
 
 
+def partition_pairs():
+    """14 blocks: block b and b + 7 are the two cost halves of the 7-block
+    partition's block b (two lane-sets: one wave per 7-block per lane-set)."""
+    global NBLK
+    nb, NBLK = NBLK, 7
+    blocks7, _ = partition()
+    NBLK = nb
+    out = [None] * 14
+    for b, blk in enumerate(blocks7):
+        h0, h1, c0, c1 = [], [], 0, 0
+        for u in sorted(blk, key=lambda u: -ucost(u)):
+            if c0 <= c1:
+                h0.append(u); c0 += ucost(u)
+            else:
+                h1.append(u); c1 += ucost(u)
+        out[b], out[b + 7] = sorted(h0), sorted(h1)
+    return out, [sum(ucost(u) for u in b) for b in out]
+
+
+def emit_shape_quad(u, u1):
+    """Four folds per cell (uint2: free apo|holo, constrained apo|holo); every
+    correction depends on the sequence only, so it is summed once (packed u32)
+    and added to both words."""
+    u2 = u - u1
+    k = kind(u1, u2)
+    L = "ldq(U.qbm, o + %d)" % u1
+    if k == "gen":
+        return "a.g%d = qmin(a.g%d, qadd(%s, gk[%d]));" % (u1 & 1, u1 & 1, L, min(abs(u1 - u2), KSAT))
+    if k == "bul":
+        return "{ const int c2 = k[%d]; a.b = qmin(a.b, qadd(%s, padd(U.ct[CT_BUL + c2], fb))); }" % (u1, L)
+    if k == "1n":
+        return "{ const int c2 = k[%d]; a.n = qmin(a.n, qadd(%s, padd(U.ct[CT_ONEN + c2], f1n))); }" % (u1, L)
+    if k in ("stk", "b1"):
+        corr = "padd(U.ct[CT_INVMM + c2], U.ct[CT_STK + C.ty8 + ((c2 * 41) >> 10)])"
+        if k == "b1":
+            corr = "padd(%s, U.fs1)" % corr
+        return "{ const int c2 = k[%d]; a.s = qmin(a.s, qadd(%s, %s)); }" % (u1, L, corr)
+    if k == "m23":
+        return ("{ const int c2 = k[%d]; a.s = qmin(a.s, qadd(%s, padd(padd(U.ct[CT_INVMM + c2], U.ct[CT_M23O + c2]), C.m23f))); }"
+                % (u1, L))
+    tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
+    return "a.s = qmin(a.s, qadd(%s, padd(U.ct[CT_INVMM + k[%d]], %s)));" % (L, u1, tab)
+
+
+ASM_CHUNK = 16   # DP reads per inline-asm batch (VGPR budget: 2 per read)
+
+
+def emit_group_quad_asm(u, out):
+    """One loop size of the four-fold kernel with the group's LDS reads in
+    inline-asm batches of ASM_CHUNK cells (the first also reads the inner-pair
+    codes and the per-size energy record), each ending in s_waitcnt
+    lgkmcnt(0): the compiler's scheduler otherwise issues these reads one at a
+    time.  The loop-correction table reads that depend on the codes and all
+    arithmetic stay in C++."""
+    shapes = list(range(u + 1))
+    spec = [u1 for u1 in shapes if kind(u1, u - u1) != "gen"]
+    need_g = any(kind(u1, u - u1) == "gen" for u1 in shapes)
+    chunks = [shapes[k:k + ASM_CHUNK] for k in range(0, len(shapes), ASM_CHUNK)]
+    for ci_, ch in enumerate(chunks):
+        outs, lines = [], []
+        for u1 in ch:
+            lines.append("ds_read_b64 %%[v%d], %%[qa] offset:%d" % (u1, 8 * u1))
+            outs.append('[v%d] "=&v"(v%d)' % (u1, u1))
+        decl = ["        uint2 %s;" % ", ".join("v%d" % u1 for u1 in ch)]
+        if ci_ == 0:
+            if spec:
+                decl.append("        uint32_t %s;" % ", ".join("c%d" % u1 for u1 in spec))
+            for u1 in spec:
+                lines.append("ds_read_u8 %%[c%d], %%[ka] offset:%d" % (u1, u1))
+                outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
+            krs = (["kr0"] if need_g else []) + (["kr1"] if u >= 2 else [])
+            if krs:
+                decl.append("        uint4 %s;" % ", ".join(krs))
+            if need_g:
+                lines.append("ds_read_b128 %%[kr0], %%[kk] offset:%d" % (32 * u))
+                outs.append('[kr0] "=&v"(kr0)')
+            if u >= 2:
+                lines.append("ds_read_b128 %%[kr1], %%[kk] offset:%d" % (32 * u + 16))
+                outs.append('[kr1] "=&v"(kr1)')
+        lines.append("s_waitcnt lgkmcnt(0)")
+        out.append("        {")
+        out.extend(decl)
+        out.append('        asm volatile(')
+        for ln in lines:
+            out.append('            "%s\\n"' % ln)
+        out.append("            : " + ", ".join(outs))
+        out.append('            : [qa] "v"(qa), [ka] "v"(ka), [kk] "v"(U.aku)')
+        out.append('            : "memory");')
+        if ci_ == 0:
+            if need_g:
+                out.append("        gk[0] = kr0.x; gk[1] = kr0.y; gk[2] = kr0.z; gk[3] = kr0.w; gk[4] = kr1.x; gk[5] = kr1.y;")
+            if u >= 2:
+                out.append("        fb = kr1.z; f1n = kr1.w;")
+            for u1 in spec:
+                out.append("        cs[%d] = c%d;" % (spec.index(u1), u1))
+        for u1 in ch:
+            u2 = u - u1
+            k = kind(u1, u2)
+            v = "v%d" % u1
+            c = "cs[%d]" % spec.index(u1) if u1 in spec else None
+            if k == "gen":
+                out.append("        a.g%d = qmin(a.g%d, qadd(%s, gk[%d]));" % (u1 & 1, u1 & 1, v, min(abs(u1 - u2), KSAT)))
+            elif k == "bul":
+                out.append("        a.b = qmin(a.b, qadd(%s, padd(U.ct[CT_BUL + %s], fb)));" % (v, c))
+            elif k == "1n":
+                out.append("        a.n = qmin(a.n, qadd(%s, padd(U.ct[CT_ONEN + %s], f1n)));" % (v, c))
+            elif k in ("stk", "b1"):
+                corr = "padd(U.ct[CT_INVMM + %s], U.ct[CT_STK + C.ty8 + ((%s * 41) >> 10)])" % (c, c)
+                if k == "b1":
+                    corr = "padd(%s, U.fs1)" % corr
+                out.append("        a.s = qmin(a.s, qadd(%s, %s));" % (v, corr))
+            elif k == "m23":
+                out.append("        a.s = qmin(a.s, qadd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));"
+                           % (v, c, c))
+            else:
+                tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
+                out.append("        a.s = qmin(a.s, qadd(%s, padd(U.ct[CT_INVMM + %s], %s)));" % (v, c, tab))
+        out.append("        }")
+    # declarations shared by the chunks go first
+    return spec, need_g
+
+
+def gen_quad():
+    blocks, load = partition_pairs()
+    out = ["// GENERATED by tools/gen_mfe_blocks.py -- do not edit.",
+           "// Interior-loop shapes of mfe_quad.hip (four folds per cell) in 14 blocks of LDS cost %s;" % load,
+           "// blocks b and b + 7 are the halves of one 7-block (two lane-sets: wave w takes both halves).",
+           "// Block b: loop sizes %s" % "; ".join("%d:%s" % (b, blk) for b, blk in enumerate(blocks)), ""]
+    for b, blk in enumerate(blocks):
+        out.append("__device__ __forceinline__ void mfq_blk%d(const QUni &U, const QCell &C, QAcc &a) {" % b)
+        out.append("    int ci = C.i, dd = U.d, um = U.umax;")
+        out.append('    asm volatile("" : "+v"(ci));')
+        out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
+        for u in blk:
+            out.append("    if (um < %d) return;" % u)
+            out.append("#ifndef MFQ_NO_ASM")
+            out.append("    {   // u = %d (batched reads)" % u)
+            out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+            out.append("        const uint32_t qa = U.aq + uint32_t(o) * 8u, ka = U.ac + uint32_t(o);")
+            nspec = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen")
+            out.append("        uint32_t gk[6], fb = 0, f1n = 0, cs[%d];" % max(1, nspec))
+            out.append("        (void)gk; (void)fb; (void)f1n; (void)cs;")
+            emit_group_quad_asm(u, out)
+            out.append("    }")
+            out.append("#else")
+            out.append("    {   // u = %d" % u)
+            out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+            out.append("        const uint2 *q = U.qbm + o;")
+            out.append("        const uint8_t *k = U.cc + o;")
+            out.append("        (void)k;")
+            need_g = any(kind(u1, u - u1) == "gen" for u1 in range(u + 1))
+            if need_g:
+                out.append("        const uint4 kr0 = U.ku[%d * 2];" % u)
+                out.append("        const uint4 kr1 = U.ku[%d * 2 + 1];" % u)
+                out.append("        const uint32_t gk[6] = {kr0.x, kr0.y, kr0.z, kr0.w, kr1.x, kr1.y};")
+                out.append("        const uint32_t fb = kr1.z, f1n = kr1.w;")
+            elif u >= 2:
+                out.append("        const uint4 kr1 = U.ku[%d * 2 + 1];" % u)
+                out.append("        const uint32_t fb = kr1.z, f1n = kr1.w;")
+                out.append("        (void)f1n;")
+            order = sorted(range(u + 1), key=lambda u1: kind(u1, u - u1) in ("i11", "i12", "i21", "i22"))
+            for u1 in order:
+                out.append("        " + emit_shape_quad(u, u1))
+            nds = (u + 1) + sum(2 if kind(u1, u - u1) not in ("gen",) else 0 for u1 in range(u + 1)) + (2 if need_g else 1)
+            out.append("        MFQ_GROUP_ORDER(%d);" % nds)
+            out.append("    }")
+            out.append("#endif")
+            out.append("    MFQ_SCHED_BARRIER();")
+        out.append("}")
+        out.append("")
+    out.append("__device__ __forceinline__ void mfq_block(int b, const QUni &U, const QCell &C, QAcc &a) {")
+    out.append("    switch (b) {")
+    for b in range(14):
+        out.append("        case %d: mfq_blk%d(U, C, a); return;" % (b, b))
+    out.append("        default: return;")
+    out.append("    }")
+    out.append("}")
+    tb = 0
+    for b, blk in enumerate(blocks):
+        if any(u in (2, 3, 4) for u in blk):
+            tb |= 1 << b
+    out.append("")
+    out.append("constexpr unsigned MFQ_TABLE_BLOCKS = 0x%xu;   // blocks with 1x1 / 1x2 / 2x1 / 2x2 shapes" % tb)
+    out.append("constexpr int MFQ_NBLK = 14;")
+    out.append("constexpr int MFQ_KSAT = %d;" % KSAT)
+    w = max(len(b) for b in blocks) + 1
+    rows = ", ".join("{" + ", ".join(str(u) for u in b + [-1] * (w - len(b))) + "}" for b in blocks)
+    out.append("// loop sizes of each block, -1 terminated (runtime path for constrained cells)")
+    out.append("__device__ constexpr int8_t MFQ_BLK_U[14][%d] = {%s};" % (w, rows))
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "addapt_amd", "csrc", "mfe_quad_blocks.inc")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+    print("quad blocks:", blocks, "load:", load, file=sys.stderr)
+
+
 def emit_shape(u, u1):
     u2 = u - u1
     k = kind(u1, u2)
@@ -173,3 +369,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    gen_quad()
