@@ -1901,15 +1901,16 @@ size_t mfe_quad_lds(const KArgs &ka);
 hipError_t launch_mfe_quad(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
                            const int *mask, hipStream_t stream);
 
-// MFE kernel choice, ADX_MFE_KERNEL: rows = score_kernel<MinPlus16> (lanes = terms),
-// cells = mfe_cells_kernel (lanes = cells, two folds per cell), quad = mfe_quad_kernel
-// (lanes = cells, four folds per cell)
+// MFE kernel choice, ADX_MFE_KERNEL: cells (default) = mfe_cells_kernel (lanes =
+// cells, two folds per cell, two walkers per CU); quad = mfe_quad_kernel (lanes =
+// cells, four folds per cell, one walker per CU: lower latency per walker, lower
+// throughput at 4096 walkers); rows = score_kernel<MinPlus16> (lanes = terms)
 static int mfe_kernel_choice() {
     static const int v = [] {
         const char *e = std::getenv("ADX_MFE_KERNEL");
-        if (e && std::strcmp(e, "cells") == 0) return 1;
+        if (e && std::strcmp(e, "rows") == 0) return 0;
         if (e && std::strcmp(e, "quad") == 0) return 2;
-        return 0;
+        return 1;
     }();
     return v;
 }

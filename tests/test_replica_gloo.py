@@ -4,6 +4,7 @@ conserved, and the acceptance rule is the detailed-balance one."""
 import math
 import os
 import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -12,6 +13,11 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from addapt_amd import replica
+
+
+def _rendezvous():
+    d = tempfile.mkdtemp(prefix="adx_gloo_")
+    return os.path.join(d, "rdzv")
 
 
 def _port():
@@ -23,9 +29,8 @@ def _port():
 
 
 def _worker(rank, world, port, W, N, rounds, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous: no port to race for when tests run in parallel
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         g = torch.Generator().manual_seed(1000 + rank)
         seqs = torch.randint(1, 5, (W, N), dtype=torch.uint8, generator=g)
@@ -36,7 +41,10 @@ def _worker(rank, world, port, W, N, rounds, q):
         stats = []
         for r in range(rounds):
             stats.append(replica.exchange_round(dist, r, rank, world, temps, seqs, scores, seed=7))
-        q.put((rank, start, (seqs, scores), stats))
+        # numpy copies travel by value (torch tensors go through shared memory that
+        # can vanish when this process exits before the parent reads the queue)
+        q.put((rank, (start[0].numpy().copy(), start[1].numpy().copy()),
+               (seqs.numpy().copy(), scores.numpy().copy()), stats))
     finally:
         dist.destroy_process_group()
 
@@ -46,7 +54,7 @@ def test_exchange_rounds_conserve_configurations(world):
     W, N, rounds = 64, 12, 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _port()
+    port = _rendezvous()
     procs = [ctx.Process(target=_worker, args=(r, world, port, W, N, rounds, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -3,12 +3,18 @@ by bench.py --gpus N: disjoint walker ids covering [0, G*W), per-walker
 initial sequences independent of G, max-over-ranks timing and counter sums."""
 import os
 import socket
+import tempfile
 
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from addapt_amd import shard, workloads
+
+
+def _rendezvous():
+    d = tempfile.mkdtemp(prefix="adx_gloo_")
+    return os.path.join(d, "rdzv")
 
 
 def _free_port():
@@ -20,9 +26,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, W, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous: no port to race for when tests run in parallel
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         ids = shard.walker_ids(rank, world, W)
         tmpl, active = workloads.synthetic(60)
@@ -38,7 +43,7 @@ def test_sharding_two_ranks():
     world, W = 2, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous()
     procs = [ctx.Process(target=_worker, args=(r, world, port, W, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -113,9 +113,10 @@ def emit_shape_quad(u, u1):
 
 
 ASM_CHUNK = 16   # DP reads per inline-asm batch (VGPR budget: 2 per read)
+ASM_CHUNK_CELLS = 24   # the same for the two-fold kernel (1 VGPR per read)
 
 
-def emit_group_quad_asm(u, out):
+def emit_group_quad_asm(u, out, cells=False):
     """One loop size of the four-fold kernel with the group's LDS reads in
     inline-asm batches of ASM_CHUNK cells (the first also reads the inner-pair
     codes and the per-size energy record), each ending in s_waitcnt
@@ -125,13 +126,16 @@ def emit_group_quad_asm(u, out):
     shapes = list(range(u + 1))
     spec = [u1 for u1 in shapes if kind(u1, u - u1) != "gen"]
     need_g = any(kind(u1, u - u1) == "gen" for u1 in shapes)
-    chunks = [shapes[k:k + ASM_CHUNK] for k in range(0, len(shapes), ASM_CHUNK)]
+    ch_n = ASM_CHUNK_CELLS if cells else ASM_CHUNK
+    chunks = [shapes[k:k + ch_n] for k in range(0, len(shapes), ch_n)]
+    vt, ld, esz = ("uint32_t", "ds_read_b32", 4) if cells else ("uint2", "ds_read_b64", 8)
+    qmin, qadd = ("pmin", "padd") if cells else ("qmin", "qadd")
     for ci_, ch in enumerate(chunks):
         outs, lines = [], []
         for u1 in ch:
-            lines.append("ds_read_b64 %%[v%d], %%[qa] offset:%d" % (u1, 8 * u1))
+            lines.append("%s %%[v%d], %%[qa] offset:%d" % (ld, u1, esz * u1))
             outs.append('[v%d] "=&v"(v%d)' % (u1, u1))
-        decl = ["        uint2 %s;" % ", ".join("v%d" % u1 for u1 in ch)]
+        decl = ["        %s %s;" % (vt, ", ".join("v%d" % u1 for u1 in ch))]
         if ci_ == 0:
             if spec:
                 decl.append("        uint32_t %s;" % ", ".join("c%d" % u1 for u1 in spec))
@@ -169,22 +173,22 @@ def emit_group_quad_asm(u, out):
             v = "v%d" % u1
             c = "cs[%d]" % spec.index(u1) if u1 in spec else None
             if k == "gen":
-                out.append("        a.g%d = qmin(a.g%d, qadd(%s, gk[%d]));" % (u1 & 1, u1 & 1, v, min(abs(u1 - u2), KSAT)))
+                out.append("        a.g%d = %s(a.g%d, %s(%s, gk[%d]));" % (u1 & 1, qmin, u1 & 1, qadd, v, min(abs(u1 - u2), KSAT)))
             elif k == "bul":
-                out.append("        a.b = qmin(a.b, qadd(%s, padd(U.ct[CT_BUL + %s], fb)));" % (v, c))
+                out.append("        a.b = %s(a.b, %s(%s, padd(U.ct[CT_BUL + %s], fb)));" % (qmin, qadd, v, c))
             elif k == "1n":
-                out.append("        a.n = qmin(a.n, qadd(%s, padd(U.ct[CT_ONEN + %s], f1n)));" % (v, c))
+                out.append("        a.n = %s(a.n, %s(%s, padd(U.ct[CT_ONEN + %s], f1n)));" % (qmin, qadd, v, c))
             elif k in ("stk", "b1"):
                 corr = "padd(U.ct[CT_INVMM + %s], U.ct[CT_STK + C.ty8 + ((%s * 41) >> 10)])" % (c, c)
                 if k == "b1":
                     corr = "padd(%s, U.fs1)" % corr
-                out.append("        a.s = qmin(a.s, qadd(%s, %s));" % (v, corr))
+                out.append("        a.s = %s(a.s, %s(%s, %s));" % (qmin, qadd, v, corr))
             elif k == "m23":
-                out.append("        a.s = qmin(a.s, qadd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));"
-                           % (v, c, c))
+                out.append("        a.s = %s(a.s, %s(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));"
+                           % (qmin, qadd, v, c, c))
             else:
                 tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
-                out.append("        a.s = qmin(a.s, qadd(%s, padd(U.ct[CT_INVMM + %s], %s)));" % (v, c, tab))
+                out.append("        a.s = %s(a.s, %s(%s, padd(U.ct[CT_INVMM + %s], %s)));" % (qmin, qadd, v, c, tab))
         out.append("        }")
     # declarations shared by the chunks go first
     return spec, need_g
@@ -305,6 +309,16 @@ def main():
         out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
         for u in blk:
             out.append("    if (um < %d) return;" % u)
+            out.append("#ifndef MFE_NO_ASM")
+            out.append("    {   // u = %d (batched reads)" % u)
+            out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+            out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
+            nspec = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen")
+            out.append("        uint32_t gk[6], fb = 0, f1n = 0, cs[%d];" % max(1, nspec))
+            out.append("        (void)gk; (void)fb; (void)f1n; (void)cs;")
+            emit_group_quad_asm(u, out, cells=True)
+            out.append("    }")
+            out.append("#else")
             out.append("    {   // u = %d" % u)
             out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
             out.append("        const uint32_t *q = U.qbm + o;")
@@ -337,6 +351,7 @@ def main():
                 if n % SCHED_CHUNK == SCHED_CHUNK - 1 and n != len(order) - 1:
                     out.append("        __builtin_amdgcn_sched_barrier(0);")
             out.append("    }")
+            out.append("#endif")
             out.append("    MFE_SCHED_BARRIER();   // bound the scheduling window (VGPR / SGPR pressure)")
         out.append("}")
         out.append("")
