@@ -85,6 +85,14 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
             "reference_2016_per_core": 14.4}
 
 
+def mfe_kernel_label():
+    """The MFE fold kernel the engine launches (kernels.hip mfe_kernel_choice)."""
+    k = os.environ.get("ADX_MFE_KERNEL", "cells")
+    return {"rows": "score_kernel<MinPlus16> (lanes = terms)",
+            "quad": "mfe_quad_kernel (lanes = cells, 4 folds per cell)"}.get(
+        k, "mfe_cells_kernel (lanes = cells, 2 folds per cell)") + " + FP32 MinPlus fallback launch"
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -186,7 +194,7 @@ def main():
         if a.fold == "pf" else
         ("fp32 VALU add/min on integer dcal energies (min-plus is not an MFMA contraction); "
          "peak = gfx950 fp32 rate"),
-        "kernel": "score_kernel<%s>" % ("MinPlus16 (+ FP32 MinPlus fallback)" if a.fold == "mfe" else "SumProd"),
+        "kernel": mfe_kernel_label() if a.fold == "mfe" else "score_kernel<SumProd>",
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": score_ms,
         "launches": launches,

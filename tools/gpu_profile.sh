@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/$tag/pmc_fetch -o fetch --output-format csv -- python bench.py --steps 3 --warmup 0 --no-cpu-baseline > gpurun_out/$tag/pmc_fetch.out 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/$tag/pmc_write -o write --output-format csv -- python bench.py --steps 3 --warmup 0 --no-cpu-baseline > gpurun_out/$tag/pmc_write.out 2>&1
 python tools/pmc_traffic.py $(find gpurun_out/$tag/pmc_fetch -name "*counter_collection.csv") $(find gpurun_out/$tag/pmc_write -name "*counter_collection.csv") > gpurun_out/$tag/traffic.json
-python tools/trace_summary.py gpurun_out/$tag/trace/bench_kernel_trace.csv --last 10 > gpurun_out/$tag/score_kernel_summary.json
+python tools/trace_summary.py $(find gpurun_out/$tag/trace -name "*kernel_trace.csv") --last 10 > gpurun_out/$tag/score_kernel_summary.json

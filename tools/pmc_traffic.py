@@ -15,11 +15,14 @@ import csv
 import json
 import sys
 
+# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip, mfe_quad.hip)
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "mfe_quad_kernel")
+
 
 def per_kernel(path, counter):
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
-        if "score_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if any(k in r["Kernel_Name"] for k in SCORE_KERNELS) and r["Counter_Name"] == counter:
             acc[r["Kernel_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     out = {}
     for name, disp in acc.items():

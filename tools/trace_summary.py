@@ -14,11 +14,14 @@ import csv
 import json
 import sys
 
+# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip, mfe_quad.hip)
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "mfe_quad_kernel")
+
 path = sys.argv[1]
 last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 10
 by = collections.defaultdict(list)
 for r in csv.DictReader(open(path)):
-    if "score_kernel" in r["Kernel_Name"]:
+    if any(k in r["Kernel_Name"] for k in SCORE_KERNELS):
         by[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 out = {"selection": "last %d launches of each score_kernel instantiation (the timed steps)" % last,
        "kernels": {}}
