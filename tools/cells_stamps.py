@@ -22,9 +22,9 @@ L.adx_debug_stamps_cells(buf, 1)
 eng.score_batch(seqs)
 L.adx_debug_stamps_cells(buf, 1)
 G = 2 * W   # fold groups
-cols = ["F", "B", "M", "Q", "barrier", "top"]
+cols = ["F", "B", "Msetup", "Mchunks", "Mtail", "Q", "barrier", "top"]
 print("cycles per fold group per wave (N=%d, W=%d, %.3f ms)" % (N, W, eng.last_kernel_ms()))
 print("wave " + " ".join("%9s" % n for n in cols))
 for w in range(8):
-    v = [buf[w * 16 + k] // G for k in (1, 2, 3, 4, 5, 0)]
+    v = [buf[w * 16 + k] // G for k in (1, 2, 6, 7, 3, 4, 5, 0)]
     print("%4d " % w + " ".join("%9d" % x for x in v))

@@ -114,6 +114,7 @@ def emit_shape_quad(u, u1):
 
 ASM_CHUNK = 16   # DP reads per inline-asm batch (VGPR budget: 2 per read)
 ASM_CHUNK_CELLS = 24   # the same for the two-fold kernel (1 VGPR per read)
+PIPE_CHUNK = 20        # pipelined two-fold blocks (pending table reads hold VGPRs)
 
 
 def emit_group_quad_asm(u, out, cells=False):
@@ -192,6 +193,178 @@ def emit_group_quad_asm(u, out, cells=False):
         out.append("        }")
     # declarations shared by the chunks go first
     return spec, need_g
+
+
+# correction-table reads of one special shape: (tag, address kind, byte offset in ct)
+CT_OFF = {"INV": 0, "BUL": 200 * 4, "ONEN": 400 * 4, "M23": 600 * 4, "STK": 800 * 4}
+
+
+def spec_reads(k):
+    if k == "bul":
+        return [("BUL", "a")]
+    if k == "1n":
+        return [("ONEN", "a")]
+    if k in ("stk", "b1"):
+        return [("INV", "a"), ("STK", "s")]
+    if k == "m23":
+        return [("INV", "a"), ("M23", "a")]
+    return [("INV", "a")]
+
+
+def spec_expr(u, u1, R):
+    """a.x = pmin(a.x, ...) of a special shape from its loaded table values R[tag]
+    (the same saturating-add order as the unpipelined path)."""
+    k = kind(u1, u - u1)
+    V = "P%d_v%d" % (u, u1)
+    if k == "bul":
+        return "a.b = pmin(a.b, padd(%s, padd(%s, P%d_fb)));" % (V, R["BUL"], u)
+    if k == "1n":
+        return "a.n = pmin(a.n, padd(%s, padd(%s, P%d_f1n)));" % (V, R["ONEN"], u)
+    if k == "stk":
+        return "a.s = pmin(a.s, padd(%s, padd(%s, %s)));" % (V, R["INV"], R["STK"])
+    if k == "b1":
+        return "a.s = pmin(a.s, padd(%s, padd(padd(%s, %s), U.fs1)));" % (V, R["INV"], R["STK"])
+    if k == "m23":
+        return "a.s = pmin(a.s, padd(%s, padd(padd(%s, %s), C.m23f)));" % (V, R["INV"], R["M23"])
+    tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
+    return "a.s = pmin(a.s, padd(%s, padd(%s, %s)));" % (V, R["INV"], tab)
+
+
+def pending_reads(u):
+    """(asm line, output binding, input binding, result name) per table read the
+    specials of group u still need; R maps (u1, tag) -> result variable."""
+    lines, outs, ins, R = [], [], set(), {}
+    for u1 in range(u + 1):
+        k = kind(u1, u - u1)
+        if k == "gen":
+            continue
+        for tag, ak in spec_reads(k):
+            r = "R%d_%d_%s" % (u, u1, tag)
+            av = "P%d_%s%d" % (u, ak, u1)
+            lines.append("ds_read_b32 %%[%s], %%[%s] offset:%d" % (r, av, CT_OFF[tag]))
+            outs.append('[%s] "=&v"(%s)' % (r, r))
+            ins.add('[%s] "v"(%s)' % (av, av))
+            R[(u1, tag)] = r
+    return lines, outs, sorted(ins), R
+
+
+def emit_pending_arith(u, R, out, ind):
+    for u1 in range(u + 1):
+        k = kind(u1, u - u1)
+        if k == "gen":
+            continue
+        out.append(ind + spec_expr(u, u1, {tag: R[(u1, tag)] for tag, _ in spec_reads(k)}))
+
+
+def emit_finish(u, out, ind):
+    """The table reads + arithmetic of group u's specials on their own."""
+    lines, outs, ins, R = pending_reads(u)
+    out.append(ind + "{")
+    out.append(ind + "    uint32_t %s;" % ", ".join(sorted(set(R.values()))))
+    out.append(ind + "    asm volatile(")
+    for ln in lines + ["s_waitcnt lgkmcnt(0)"]:
+        out.append(ind + '        "%s\\n"' % ln)
+    out.append(ind + "        : " + ", ".join(outs))
+    out.append(ind + "        : " + ", ".join(ins))
+    out.append(ind + '        : "memory");')
+    emit_pending_arith(u, R, out, ind + "    ")
+    out.append(ind + "}")
+
+
+def emit_block_cells_pipe(blk, out):
+    """Inline-asm path of one block with the correction-table reads of group g
+    (they depend on the inner-pair codes group g's batch returns) issued in
+    group g+1's batch: one LDS round trip per loop size instead of two."""
+    prev = None
+    for u in blk:
+        spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen"]
+        need_g = len(spec) < u + 1
+        if prev is None:
+            out.append("    if (um < %d) return;" % u)
+        else:
+            out.append("    if (um < %d) {" % u)
+            emit_finish(prev, out, "        ")
+            out.append("        return;")
+            out.append("    }")
+        decl = []
+        for u1 in spec:
+            decl += ["P%d_v%d" % (u, u1), "P%d_a%d" % (u, u1)]
+            if kind(u1, u - u1) in ("stk", "b1"):
+                decl.append("P%d_s%d" % (u, u1))
+        if any(kind(u1, u - u1) == "bul" for u1 in spec):
+            decl.append("P%d_fb" % u)
+        if any(kind(u1, u - u1) == "1n" for u1 in spec):
+            decl.append("P%d_f1n" % u)
+        out.append("    uint32_t %s;   // group u = %d: pending specials" % (", ".join(decl), u))
+        out.append("    {   // u = %d (batched reads%s)" % (u, "" if prev is None else " + the table reads of u = %d" % prev))
+        out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+        out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
+        if need_g:
+            out.append("        uint32_t gk[6];")
+        shapes = list(range(u + 1))
+        chunks = [shapes[k:k + PIPE_CHUNK] for k in range(0, len(shapes), PIPE_CHUNK)]
+        for ci_, ch in enumerate(chunks):
+            lines, outs, ins = [], [], ['[qa] "v"(qa)']
+            decl = ["        uint32_t %s;" % ", ".join("v%d" % u1 for u1 in ch)]
+            for u1 in ch:
+                lines.append("ds_read_b32 %%[v%d], %%[qa] offset:%d" % (u1, 4 * u1))
+                outs.append('[v%d] "=&v"(v%d)' % (u1, u1))
+            R = {}
+            if ci_ == 0:
+                ins += ['[ka] "v"(ka)', '[kk] "v"(U.aku)']
+                if spec:
+                    decl.append("        uint32_t %s;" % ", ".join("c%d" % u1 for u1 in spec))
+                for u1 in spec:
+                    lines.append("ds_read_u8 %%[c%d], %%[ka] offset:%d" % (u1, u1))
+                    outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
+                krs = (["kr0"] if need_g else []) + (["kr1"] if u >= 2 else [])
+                if krs:
+                    decl.append("        uint4 %s;" % ", ".join(krs))
+                if need_g:
+                    lines.append("ds_read_b128 %%[kr0], %%[kk] offset:%d" % (32 * u))
+                    outs.append('[kr0] "=&v"(kr0)')
+                if u >= 2:
+                    lines.append("ds_read_b128 %%[kr1], %%[kk] offset:%d" % (32 * u + 16))
+                    outs.append('[kr1] "=&v"(kr1)')
+            if prev is not None and ci_ == len(chunks) - 1:   # in the smallest (last) batch
+                pl, po, pi, R = pending_reads(prev)
+                decl.append("        uint32_t %s;" % ", ".join(sorted(set(R.values()))))
+                lines += pl
+                outs += po
+                ins += pi
+            lines.append("s_waitcnt lgkmcnt(0)")
+            out.append("        {")
+            out.extend(decl)
+            out.append("        asm volatile(")
+            for ln in lines:
+                out.append('            "%s\\n"' % ln)
+            out.append("            : " + ", ".join(outs))
+            out.append("            : " + ", ".join(ins))
+            out.append('            : "memory");')
+            if R:
+                emit_pending_arith(prev, R, out, "        ")
+            if ci_ == 0:
+                if need_g:
+                    out.append("        gk[0] = kr0.x; gk[1] = kr0.y; gk[2] = kr0.z; gk[3] = kr0.w; gk[4] = kr1.x; gk[5] = kr1.y;")
+                if any(kind(u1, u - u1) == "bul" for u1 in spec):
+                    out.append("        P%d_fb = kr1.z;" % u)
+                if any(kind(u1, u - u1) == "1n" for u1 in spec):
+                    out.append("        P%d_f1n = kr1.w;" % u)
+                for u1 in spec:
+                    out.append("        P%d_a%d = U.act + c%d * 4u;" % (u, u1, u1))
+                    if kind(u1, u - u1) in ("stk", "b1"):
+                        out.append("        P%d_s%d = U.act + uint32_t(C.ty8 + ((c%d * 41) >> 10)) * 4u;" % (u, u1, u1))
+            for u1 in ch:
+                u2 = u - u1
+                if kind(u1, u2) == "gen":
+                    out.append("        a.g%d = pmin(a.g%d, padd(v%d, gk[%d]));" % (u1 & 1, u1 & 1, u1, min(abs(u1 - u2), KSAT)))
+                else:
+                    out.append("        P%d_v%d = v%d;" % (u, u1, u1))
+            out.append("        }")
+        out.append("    }")
+        out.append("    MFE_SCHED_BARRIER();   // bound the scheduling window (VGPR / SGPR pressure)")
+        prev = u
+    emit_finish(prev, out, "    ")
 
 
 def gen_quad():
@@ -307,9 +480,11 @@ def main():
         out.append("    int ci = C.i, dd = U.d, um = U.umax;")
         out.append('    asm volatile("" : "+v"(ci));')
         out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
+        out.append("#if defined(MFE_PIPE) && !defined(MFE_NO_ASM)   // table reads one group late (measured slower)")
+        emit_block_cells_pipe(blk, out)
+        out.append("#elif !defined(MFE_NO_ASM)")
         for u in blk:
             out.append("    if (um < %d) return;" % u)
-            out.append("#ifndef MFE_NO_ASM")
             out.append("    {   // u = %d (batched reads)" % u)
             out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
             out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
@@ -318,7 +493,10 @@ def main():
             out.append("        (void)gk; (void)fb; (void)f1n; (void)cs;")
             emit_group_quad_asm(u, out, cells=True)
             out.append("    }")
-            out.append("#else")
+            out.append("    MFE_SCHED_BARRIER();   // bound the scheduling window (VGPR / SGPR pressure)")
+        out.append("#else")
+        for u in blk:
+            out.append("    if (um < %d) return;" % u)
             out.append("    {   // u = %d" % u)
             out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
             out.append("        const uint32_t *q = U.qbm + o;")
@@ -351,8 +529,8 @@ def main():
                 if n % SCHED_CHUNK == SCHED_CHUNK - 1 and n != len(order) - 1:
                     out.append("        __builtin_amdgcn_sched_barrier(0);")
             out.append("    }")
-            out.append("#endif")
             out.append("    MFE_SCHED_BARRIER();   // bound the scheduling window (VGPR / SGPR pressure)")
+        out.append("#endif")
         out.append("}")
         out.append("")
     out.append("__device__ __forceinline__ void mfe_block(int b, const BUni &U, const BCell &C, Acc &a) {")
