@@ -117,7 +117,10 @@ ASM_CHUNK_CELLS = 24   # the same for the two-fold kernel (1 VGPR per read)
 PIPE_CHUNK = 20        # pipelined two-fold blocks (pending table reads hold VGPRs)
 
 
-def emit_group_quad_asm(u, out, cells=False):
+TABK = ("i11", "i12", "i21", "i22")
+
+
+def emit_group_quad_asm(u, out, cells=False, defer=False):
     """One loop size of the four-fold kernel with the group's LDS reads in
     inline-asm batches of ASM_CHUNK cells (the first also reads the inner-pair
     codes and the per-size energy record), each ending in s_waitcnt
@@ -187,6 +190,8 @@ def emit_group_quad_asm(u, out, cells=False):
             elif k == "m23":
                 out.append("        a.s = %s(a.s, %s(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));"
                            % (qmin, qadd, v, c, c))
+            elif defer:   # the HBM table value lands later: finish at the block end
+                out.append("        tv_%s = %s; ti_%s = U.ct[CT_INVMM + %s];" % (k, v, k, c))
             else:
                 tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
                 out.append("        a.s = %s(a.s, %s(%s, padd(U.ct[CT_INVMM + %s], %s)));" % (qmin, qadd, v, c, tab))
@@ -367,6 +372,118 @@ def emit_block_cells_pipe(blk, out):
     emit_finish(prev, out, "    ")
 
 
+def table_kinds(blk):
+    return sorted({kind(u1, u - u1) for u in blk for u1 in range(u + 1)} & set(TABK))
+
+
+def emit_table_decl(blk, out):
+    """1x1 .. 2x2 shapes wait for their HBM table values until the block end."""
+    for k in table_kinds(blk):
+        out.append("    u32 tv_%s = INF16, ti_%s = 0u;" % (k, k))
+
+
+def emit_table_fin(blk, out):
+    out.append("fin:")
+    for k in table_kinds(blk):
+        tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
+        out.append("    a.s = pmin(a.s, padd(tv_%s, padd(ti_%s, %s)));" % (k, k, tab))
+    out.append("    return;")
+
+
+def emit_block_cells_sliced(blk, S, out):
+    """Inline-asm path of one block with S lanes per cell (S = 2, 4): lane slice
+    r = 0..S-1 reads the generic shapes u1 = 2 + r + S*k of each loop size (one
+    per-lane base + immediate offsets), so a diagonal with <= 64/S pairable cells
+    runs the generic shapes in 1/S of the instructions.  Every slice also runs
+    the special shapes (counting a shape in several slices leaves the minimum
+    unchanged); the caller folds a.g0 / a.g1 across the slices."""
+    for u in blk:
+        out.append("    if (um < %d) goto fin;" % u)
+        spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen"]
+        gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
+        out.append("    {   // u = %d (%d slices)" % (u, S))
+        out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+        out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
+        lines, outs, ins = [], [], ['[qa] "v"(qa)', '[ka] "v"(ka)', '[kk] "v"(U.aku)']
+        decl = []
+        if spec:
+            decl.append("        uint32_t %s;" % ", ".join("v%d" % u1 for u1 in spec))
+            decl.append("        uint32_t %s;" % ", ".join("c%d" % u1 for u1 in spec))
+        for u1 in spec:
+            lines.append("ds_read_b32 %%[v%d], %%[qa] offset:%d" % (u1, 4 * u1))
+            outs.append('[v%d] "=&v"(v%d)' % (u1, u1))
+        for u1 in spec:
+            lines.append("ds_read_u8 %%[c%d], %%[ka] offset:%d" % (u1, u1))
+            outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
+        nk = 0
+        if gen:
+            g0 = gen[0]
+            nk = (len(gen) + S - 1) // S
+            out.append("        const uint32_t qg = qa + C.rs + %du;   // this slice's first generic shape" % (4 * g0))
+            ins.append('[qg] "v"(qg)')
+            decl.append("        uint32_t %s;" % ", ".join("w%d" % k for k in range(nk)))
+            for k in range(nk):
+                lines.append("ds_read_b32 %%[w%d], %%[qg] offset:%d" % (k, 4 * S * k))
+                outs.append('[w%d] "=&v"(w%d)' % (k, k))
+        krs = (["kr0"] if gen else []) + (["kr1"] if u >= 2 else [])
+        if krs:
+            decl.append("        uint4 %s;" % ", ".join(krs))
+        if gen:
+            lines.append("ds_read_b128 %%[kr0], %%[kk] offset:%d" % (32 * u))
+            outs.append('[kr0] "=&v"(kr0)')
+        if u >= 2:
+            lines.append("ds_read_b128 %%[kr1], %%[kk] offset:%d" % (32 * u + 16))
+            outs.append('[kr1] "=&v"(kr1)')
+        lines.append("s_waitcnt lgkmcnt(0)")
+        out.extend(decl)
+        out.append("        asm volatile(")
+        for ln in lines:
+            out.append('            "%s\\n"' % ln)
+        out.append("            : " + ", ".join(outs))
+        out.append("            : " + ", ".join(ins))
+        out.append('            : "memory");')
+        if gen:
+            out.append("        const uint32_t gk[6] = {kr0.x, kr0.y, kr0.z, kr0.w, kr1.x, kr1.y};")
+        if u >= 2:
+            out.append("        const uint32_t fb = kr1.z, f1n = kr1.w;")
+            out.append("        (void)fb; (void)f1n;")
+        for u1 in spec:
+            u2 = u - u1
+            k = kind(u1, u2)
+            v, c = "v%d" % u1, "c%d" % u1
+            if k == "bul":
+                out.append("        a.b = pmin(a.b, padd(%s, padd(U.ct[CT_BUL + %s], fb)));" % (v, c))
+            elif k == "1n":
+                out.append("        a.n = pmin(a.n, padd(%s, padd(U.ct[CT_ONEN + %s], f1n)));" % (v, c))
+            elif k in ("stk", "b1"):
+                corr = "padd(U.ct[CT_INVMM + %s], U.ct[CT_STK + C.ty8 + ((%s * 41) >> 10)])" % (c, c)
+                if k == "b1":
+                    corr = "padd(%s, U.fs1)" % corr
+                out.append("        a.s = pmin(a.s, padd(%s, %s));" % (v, corr))
+            elif k == "m23":
+                out.append("        a.s = pmin(a.s, padd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));" % (v, c, c))
+            else:
+                out.append("        tv_%s = %s; ti_%s = U.ct[CT_INVMM + %s];" % (k, v, k, c))
+        for k in range(nk):
+            vals = []
+            for r in range(S):
+                u1 = g0 + r + S * k
+                if u1 in gen:
+                    vals.append("gk[%d]" % min(abs(2 * u1 - u), KSAT))
+                else:
+                    vals.append("INF16")
+            if len(set(vals)) == 1:
+                e = vals[0]
+            elif S == 2:
+                e = "(C.r1 ? %s : %s)" % (vals[1], vals[0])
+            else:
+                e = "(C.r2 ? (C.r1 ? %s : %s) : (C.r1 ? %s : %s))" % (vals[3], vals[2], vals[1], vals[0])
+            out.append("        a.g%d = pmin(a.g%d, padd(w%d, %s));" % (k & 1, k & 1, k, e))
+        out.append("    }")
+        out.append("    MFE_SCHED_BARRIER();")
+    emit_table_fin(blk, out)
+
+
 def gen_quad():
     blocks, load = partition_pairs()
     out = ["// GENERATED by tools/gen_mfe_blocks.py -- do not edit.",
@@ -483,17 +600,19 @@ def main():
         out.append("#if defined(MFE_PIPE) && !defined(MFE_NO_ASM)   // table reads one group late (measured slower)")
         emit_block_cells_pipe(blk, out)
         out.append("#elif !defined(MFE_NO_ASM)")
+        emit_table_decl(blk, out)
         for u in blk:
-            out.append("    if (um < %d) return;" % u)
+            out.append("    if (um < %d) goto fin;" % u)
             out.append("    {   // u = %d (batched reads)" % u)
             out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
             out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
             nspec = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen")
             out.append("        uint32_t gk[6], fb = 0, f1n = 0, cs[%d];" % max(1, nspec))
             out.append("        (void)gk; (void)fb; (void)f1n; (void)cs;")
-            emit_group_quad_asm(u, out, cells=True)
+            emit_group_quad_asm(u, out, cells=True, defer=True)
             out.append("    }")
             out.append("    MFE_SCHED_BARRIER();   // bound the scheduling window (VGPR / SGPR pressure)")
+        emit_table_fin(blk, out)
         out.append("#else")
         for u in blk:
             out.append("    if (um < %d) return;" % u)
@@ -541,6 +660,26 @@ def main():
     out.append("    }")
     out.append("}")
     out.append("")
+    out.append("#ifndef MFE_NO_ASM")
+    for S in (2, 4):
+        for b, blk in enumerate(blocks):
+            out.append("__device__ __forceinline__ void mfe_blk%d_s%d(const BUni &U, const BCell &C, Acc &a) {" % (b, S))
+            out.append("    int ci = C.i, dd = U.d, um = U.umax;")
+            out.append('    asm volatile("" : "+v"(ci));')
+            out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
+            emit_table_decl(blk, out)
+            emit_block_cells_sliced(blk, S, out)
+            out.append("}")
+            out.append("")
+        out.append("__device__ __forceinline__ void mfe_block_s%d(int b, const BUni &U, const BCell &C, Acc &a) {" % S)
+        out.append("    switch (b) {")
+        for b in range(NBLK):
+            out.append("        case %d: mfe_blk%d_s%d(U, C, a); return;" % (b, b, S))
+        out.append("        default: return;")
+        out.append("    }")
+        out.append("}")
+        out.append("")
+    out.append("#endif")
     # which blocks hold the table shapes (prefetch only there)
     tb = 0
     for b, blk in enumerate(blocks):
