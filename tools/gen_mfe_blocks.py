@@ -120,6 +120,27 @@ PIPE_CHUNK = 20        # pipelined two-fold blocks (pending table reads hold VGP
 TABK = ("i11", "i12", "i21", "i22")
 
 
+def plateau_min(vals, e, ind):
+    """Generic shapes with the saturated (plateau) energy e: a pairwise min tree,
+    then one add (no saturation for possible values, and stored impossible
+    values stay impossible: the same result as adding first)."""
+    vals = list(vals)
+    lines = []
+    n = 0
+    while len(vals) > 1:
+        nxt = []
+        for a in range(0, len(vals) - 1, 2):
+            t = "pm%d" % n
+            n += 1
+            lines.append(ind + "const u32 %s = pmin(%s, %s);" % (t, vals[a], vals[a + 1]))
+            nxt.append(t)
+        if len(vals) % 2:
+            nxt.append(vals[-1])
+        vals = nxt
+    lines.append(ind + "a.g0 = pmin(a.g0, padd(%s, %s));" % (vals[0], e))
+    return ["        {"] + lines + ["        }"] if False else [ind[:-4] + "{"] + lines + [ind[:-4] + "}"]
+
+
 def emit_group_quad_asm(u, out, cells=False, defer=False):
     """One loop size of the four-fold kernel with the group's LDS reads in
     inline-asm batches of ASM_CHUNK cells (the first also reads the inner-pair
@@ -171,12 +192,15 @@ def emit_group_quad_asm(u, out, cells=False, defer=False):
                 out.append("        fb = kr1.z; f1n = kr1.w;")
             for u1 in spec:
                 out.append("        cs[%d] = c%d;" % (spec.index(u1), u1))
+        pl = []
         for u1 in ch:
             u2 = u - u1
             k = kind(u1, u2)
             v = "v%d" % u1
             c = "cs[%d]" % spec.index(u1) if u1 in spec else None
-            if k == "gen":
+            if k == "gen" and cells and abs(u1 - u2) >= KSAT:   # plateau: min first, add once
+                pl.append(v)
+            elif k == "gen":
                 out.append("        a.g%d = %s(a.g%d, %s(%s, gk[%d]));" % (u1 & 1, qmin, u1 & 1, qadd, v, min(abs(u1 - u2), KSAT)))
             elif k == "bul":
                 out.append("        a.b = %s(a.b, %s(%s, padd(U.ct[CT_BUL + %s], fb)));" % (qmin, qadd, v, c))
@@ -195,6 +219,8 @@ def emit_group_quad_asm(u, out, cells=False, defer=False):
             else:
                 tab = {"i11": "C.t11", "i12": "C.t12", "i21": "C.t21", "i22": "C.t22"}[k]
                 out.append("        a.s = %s(a.s, %s(%s, padd(U.ct[CT_INVMM + %s], %s)));" % (qmin, qadd, v, c, tab))
+        if pl:
+            out.extend(plateau_min(pl, "gk[%d]" % KSAT, "        "))
         out.append("        }")
     # declarations shared by the chunks go first
     return spec, need_g
@@ -390,97 +416,142 @@ def emit_table_fin(blk, out):
     out.append("    return;")
 
 
+MERGE_SLICED = 0   # two loop sizes share a read batch while their reads fit this many VGPRs
+
+
+def sliced_regs(u, S):
+    spec = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen")
+    ngen = u + 1 - spec
+    return 2 * spec + (ngen + S - 1) // S + 4 * ((1 if ngen else 0) + (1 if u >= 2 else 0))
+
+
+def sliced_parts(u, S, t):
+    """One loop size of a sliced block, variable names suffixed by t: address
+    lines, declarations, asm reads/outputs/inputs and the arithmetic after the
+    batch."""
+    spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen"]
+    gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
+    pre, decl, lines, outs, ins, post = [], [], [], [], [], []
+    pre.append("const int o%s = off(dd - %d, U.N) + ci;" % (t, u + 2))
+    pre.append("const uint32_t qa%s = U.aq + uint32_t(o%s) * 4u, ka%s = U.ac + uint32_t(o%s);" % (t, t, t, t))
+    ins += ['[qa%s] "v"(qa%s)' % (t, t), '[ka%s] "v"(ka%s)' % (t, t)]
+    V = lambda u1: "v%d%s" % (u1, t)
+    Cc = lambda u1: "c%d%s" % (u1, t)
+    decl.append("uint32_t %s;" % ", ".join(V(u1) for u1 in spec))
+    decl.append("uint32_t %s;" % ", ".join(Cc(u1) for u1 in spec))
+    for u1 in spec:
+        lines.append("ds_read_b32 %%[%s], %%[qa%s] offset:%d" % (V(u1), t, 4 * u1))
+        outs.append('[%s] "=&v"(%s)' % (V(u1), V(u1)))
+    for u1 in spec:
+        lines.append("ds_read_u8 %%[%s], %%[ka%s] offset:%d" % (Cc(u1), t, u1))
+        outs.append('[%s] "=&v"(%s)' % (Cc(u1), Cc(u1)))
+    nk = 0
+    if gen:
+        g0 = gen[0]
+        nk = (len(gen) + S - 1) // S
+        pre.append("const uint32_t qg%s = qa%s + C.rs + %du;   // this slice's first generic shape" % (t, t, 4 * g0))
+        ins.append('[qg%s] "v"(qg%s)' % (t, t))
+        decl.append("uint32_t %s;" % ", ".join("w%d%s" % (k, t) for k in range(nk)))
+        for k in range(nk):
+            lines.append("ds_read_b32 %%[w%d%s], %%[qg%s] offset:%d" % (k, t, t, 4 * S * k))
+            outs.append('[w%d%s] "=&v"(w%d%s)' % (k, t, k, t))
+    krs = (["kr0" + t] if gen else []) + (["kr1" + t] if u >= 2 else [])
+    if krs:
+        decl.append("uint4 %s;" % ", ".join(krs))
+    if gen:
+        lines.append("ds_read_b128 %%[kr0%s], %%[kk] offset:%d" % (t, 32 * u))
+        outs.append('[kr0%s] "=&v"(kr0%s)' % (t, t))
+    if u >= 2:
+        lines.append("ds_read_b128 %%[kr1%s], %%[kk] offset:%d" % (t, 32 * u + 16))
+        outs.append('[kr1%s] "=&v"(kr1%s)' % (t, t))
+    if gen:
+        post.append("const uint32_t gk%s[6] = {kr0%s.x, kr0%s.y, kr0%s.z, kr0%s.w, kr1%s.x, kr1%s.y};" % ((t,) * 7))
+    if u >= 2:
+        post.append("const uint32_t fb%s = kr1%s.z, f1n%s = kr1%s.w;" % (t, t, t, t))
+        post.append("(void)fb%s; (void)f1n%s;" % (t, t))
+    for u1 in spec:
+        k = kind(u1, u - u1)
+        v, c = V(u1), Cc(u1)
+        if k == "bul":
+            post.append("a.b = pmin(a.b, padd(%s, padd(U.ct[CT_BUL + %s], fb%s)));" % (v, c, t))
+        elif k == "1n":
+            post.append("a.n = pmin(a.n, padd(%s, padd(U.ct[CT_ONEN + %s], f1n%s)));" % (v, c, t))
+        elif k in ("stk", "b1"):
+            corr = "padd(U.ct[CT_INVMM + %s], U.ct[CT_STK + C.ty8 + ((%s * 41) >> 10)])" % (c, c)
+            if k == "b1":
+                corr = "padd(%s, U.fs1)" % corr
+            post.append("a.s = pmin(a.s, padd(%s, %s));" % (v, corr))
+        elif k == "m23":
+            post.append("a.s = pmin(a.s, padd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));" % (v, c, c))
+        else:
+            post.append("tv_%s = %s; ti_%s = U.ct[CT_INVMM + %s];" % (k, v, k, c))
+    pl = []
+    for k in range(nk):
+        vals = []
+        for r in range(S):
+            u1 = gen[0] + r + S * k
+            vals.append("gk%s[%d]" % (t, min(abs(2 * u1 - u), KSAT)) if u1 in gen else "INF16")
+        if len(set(vals)) == 1 and vals[0] == "gk%s[%d]" % (t, KSAT):
+            pl.append("w%d%s" % (k, t))
+            continue
+        if len(set(vals)) == 1:
+            e = vals[0]
+        elif S == 2:
+            e = "(C.r1 ? %s : %s)" % (vals[1], vals[0])
+        else:
+            e = "(C.r2 ? (C.r1 ? %s : %s) : (C.r1 ? %s : %s))" % (vals[3], vals[2], vals[1], vals[0])
+        post.append("a.g%d = pmin(a.g%d, padd(w%d%s, %s));" % (k & 1, k & 1, k, t, e))
+    if pl:
+        post.extend(x.strip() for x in plateau_min(pl, "gk%s[%d]" % (t, KSAT), "    "))
+    return pre, decl, lines, outs, ins, post
+
+
+def emit_sliced_batch(groups, S, out, ind):
+    """One inline-asm read batch for the loop sizes in groups, then their arithmetic."""
+    parts = [sliced_parts(u, S, t) for u, t in groups]
+    out.append(ind + "{   // u = %s (%d slices)" % (", ".join(str(u) for u, _ in groups), S))
+    for p in parts:
+        out.extend(ind + "    " + x for x in p[0] + p[1])
+    lines = sum((p[2] for p in parts), []) + ["s_waitcnt lgkmcnt(0)"]
+    outs = sum((p[3] for p in parts), [])
+    ins = sum((p[4] for p in parts), []) + ['[kk] "v"(U.aku)']
+    out.append(ind + "    asm volatile(")
+    for ln in lines:
+        out.append(ind + '        "%s\\n"' % ln)
+    out.append(ind + "        : " + ", ".join(outs))
+    out.append(ind + "        : " + ", ".join(ins))
+    out.append(ind + '        : "memory");')
+    for p in parts:
+        out.extend(ind + "    " + x for x in p[5])
+    out.append(ind + "}")
+    out.append(ind + "MFE_SCHED_BARRIER();")
+
+
 def emit_block_cells_sliced(blk, S, out):
     """Inline-asm path of one block with S lanes per cell (S = 2, 4): lane slice
     r = 0..S-1 reads the generic shapes u1 = 2 + r + S*k of each loop size (one
     per-lane base + immediate offsets), so a diagonal with <= 64/S pairable cells
     runs the generic shapes in 1/S of the instructions.  Every slice also runs
     the special shapes (counting a shape in several slices leaves the minimum
-    unchanged); the caller folds a.g0 / a.g1 across the slices."""
-    for u in blk:
-        out.append("    if (um < %d) goto fin;" % u)
-        spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen"]
-        gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
-        out.append("    {   // u = %d (%d slices)" % (u, S))
-        out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
-        out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
-        lines, outs, ins = [], [], ['[qa] "v"(qa)', '[ka] "v"(ka)', '[kk] "v"(U.aku)']
-        decl = []
-        if spec:
-            decl.append("        uint32_t %s;" % ", ".join("v%d" % u1 for u1 in spec))
-            decl.append("        uint32_t %s;" % ", ".join("c%d" % u1 for u1 in spec))
-        for u1 in spec:
-            lines.append("ds_read_b32 %%[v%d], %%[qa] offset:%d" % (u1, 4 * u1))
-            outs.append('[v%d] "=&v"(v%d)' % (u1, u1))
-        for u1 in spec:
-            lines.append("ds_read_u8 %%[c%d], %%[ka] offset:%d" % (u1, u1))
-            outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
-        nk = 0
-        if gen:
-            g0 = gen[0]
-            nk = (len(gen) + S - 1) // S
-            out.append("        const uint32_t qg = qa + C.rs + %du;   // this slice's first generic shape" % (4 * g0))
-            ins.append('[qg] "v"(qg)')
-            decl.append("        uint32_t %s;" % ", ".join("w%d" % k for k in range(nk)))
-            for k in range(nk):
-                lines.append("ds_read_b32 %%[w%d], %%[qg] offset:%d" % (k, 4 * S * k))
-                outs.append('[w%d] "=&v"(w%d)' % (k, k))
-        krs = (["kr0"] if gen else []) + (["kr1"] if u >= 2 else [])
-        if krs:
-            decl.append("        uint4 %s;" % ", ".join(krs))
-        if gen:
-            lines.append("ds_read_b128 %%[kr0], %%[kk] offset:%d" % (32 * u))
-            outs.append('[kr0] "=&v"(kr0)')
-        if u >= 2:
-            lines.append("ds_read_b128 %%[kr1], %%[kk] offset:%d" % (32 * u + 16))
-            outs.append('[kr1] "=&v"(kr1)')
-        lines.append("s_waitcnt lgkmcnt(0)")
-        out.extend(decl)
-        out.append("        asm volatile(")
-        for ln in lines:
-            out.append('            "%s\\n"' % ln)
-        out.append("            : " + ", ".join(outs))
-        out.append("            : " + ", ".join(ins))
-        out.append('            : "memory");')
-        if gen:
-            out.append("        const uint32_t gk[6] = {kr0.x, kr0.y, kr0.z, kr0.w, kr1.x, kr1.y};")
-        if u >= 2:
-            out.append("        const uint32_t fb = kr1.z, f1n = kr1.w;")
-            out.append("        (void)fb; (void)f1n;")
-        for u1 in spec:
-            u2 = u - u1
-            k = kind(u1, u2)
-            v, c = "v%d" % u1, "c%d" % u1
-            if k == "bul":
-                out.append("        a.b = pmin(a.b, padd(%s, padd(U.ct[CT_BUL + %s], fb)));" % (v, c))
-            elif k == "1n":
-                out.append("        a.n = pmin(a.n, padd(%s, padd(U.ct[CT_ONEN + %s], f1n)));" % (v, c))
-            elif k in ("stk", "b1"):
-                corr = "padd(U.ct[CT_INVMM + %s], U.ct[CT_STK + C.ty8 + ((%s * 41) >> 10)])" % (c, c)
-                if k == "b1":
-                    corr = "padd(%s, U.fs1)" % corr
-                out.append("        a.s = pmin(a.s, padd(%s, %s));" % (v, corr))
-            elif k == "m23":
-                out.append("        a.s = pmin(a.s, padd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));" % (v, c, c))
-            else:
-                out.append("        tv_%s = %s; ti_%s = U.ct[CT_INVMM + %s];" % (k, v, k, c))
-        for k in range(nk):
-            vals = []
-            for r in range(S):
-                u1 = g0 + r + S * k
-                if u1 in gen:
-                    vals.append("gk[%d]" % min(abs(2 * u1 - u), KSAT))
-                else:
-                    vals.append("INF16")
-            if len(set(vals)) == 1:
-                e = vals[0]
-            elif S == 2:
-                e = "(C.r1 ? %s : %s)" % (vals[1], vals[0])
-            else:
-                e = "(C.r2 ? (C.r1 ? %s : %s) : (C.r1 ? %s : %s))" % (vals[3], vals[2], vals[1], vals[0])
-            out.append("        a.g%d = pmin(a.g%d, padd(w%d, %s));" % (k & 1, k & 1, k, e))
-        out.append("    }")
-        out.append("    MFE_SCHED_BARRIER();")
+    unchanged); the caller folds a.g0 / a.g1 across the slices.  Consecutive
+    loop sizes share one read batch (one LDS round trip for two sizes) once the
+    span admits both."""
+    k = 0
+    while k < len(blk):
+        if k + 1 < len(blk) and sliced_regs(blk[k], S) + sliced_regs(blk[k + 1], S) <= MERGE_SLICED:
+            ua, ub = blk[k], blk[k + 1]
+            out.append("    if (um < %d) goto fin;" % ua)
+            out.append("    if (um >= %d) {" % ub)
+            emit_sliced_batch([(ua, "a"), (ub, "b")], S, out, "        ")
+            out.append("    } else {")
+            emit_sliced_batch([(ua, "a")], S, out, "        ")
+            out.append("        goto fin;")
+            out.append("    }")
+            k += 2
+        else:
+            out.append("    if (um < %d) goto fin;" % blk[k])
+            emit_sliced_batch([(blk[k], "a")], S, out, "    ")
+            k += 1
     emit_table_fin(blk, out)
 
 
