@@ -25,6 +25,6 @@ G = 2 * W   # fold groups
 cols = ["F", "B", "Msetup", "Mchunks", "Mtail", "Q", "barrier", "top"]
 print("cycles per fold group per wave (N=%d, W=%d, %.3f ms)" % (N, W, eng.last_kernel_ms()))
 print("wave " + " ".join("%9s" % n for n in cols))
-for w in range(8):
+for w in range(int(os.environ.get("ADX_NWV", "10"))):
     v = [buf[w * 16 + k] // G for k in (1, 2, 6, 7, 3, 4, 5, 0)]
     print("%4d " % w + " ".join("%9d" % x for x in v))
