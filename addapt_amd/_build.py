@@ -37,7 +37,9 @@ def _run(cmd):
 def build_gpu(force=False):
     os.makedirs(OBJ, exist_ok=True)
     lib = os.path.join(OUT, "libaddapt_gpu.so")
-    headers = glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "addapt_gpu.h")]
+    # generated shape blocks (*.inc) are included by the kernels: a change must rebuild them
+    headers = (glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.inc")) +
+               [os.path.join(ROOT, "include", "addapt_gpu.h")])
     jobs = []
     objs = []
     for src in GPU_SOURCES:
