@@ -23,6 +23,12 @@ Shape kinds (accumulator):
 import os
 import sys
 
+def out_dir():
+    """addapt_amd/csrc, or ADX_GEN_OUT (tests regenerate into a scratch directory)."""
+    return os.environ.get("ADX_GEN_OUT") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "addapt_amd", "csrc")
+
+
 MAXLOOP = 30
 NBLK = 7           # waves 0..6 (wave 7 folds the multiloop qm / mla)
 SCHED_CHUNK = 1000 # shapes per scheduling window (whole loop sizes)
@@ -622,8 +628,7 @@ def gen_quad():
     rows = ", ".join("{" + ", ".join(str(u) for u in b + [-1] * (w - len(b))) + "}" for b in blocks)
     out.append("// loop sizes of each block, -1 terminated (runtime path for constrained cells)")
     out.append("__device__ constexpr int8_t MFQ_BLK_U[14][%d] = {%s};" % (w, rows))
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "addapt_amd", "csrc", "mfe_quad_blocks.inc")
+    path = os.path.join(out_dir(), "mfe_quad_blocks.inc")
     with open(path, "w") as f:
         f.write("\n".join(out) + "\n")
     print("quad blocks:", blocks, "load:", load, file=sys.stderr)
@@ -763,8 +768,7 @@ def main():
     rows = ", ".join("{" + ", ".join(str(u) for u in b + [-1] * (w - len(b))) + "}" for b in blocks)
     out.append("// loop sizes of each block, -1 terminated (runtime path for constrained cells)")
     out.append("__device__ constexpr int8_t MFE_BLK_U[%d][%d] = {%s};" % (NBLK, w, rows))
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "addapt_amd", "csrc", "mfe_blocks.inc")
+    path = os.path.join(out_dir(), "mfe_blocks.inc")
     with open(path, "w") as f:
         f.write("\n".join(out) + "\n")
     print("blocks:", blocks, "load:", load, file=sys.stderr)
