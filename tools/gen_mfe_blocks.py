@@ -191,6 +191,12 @@ def emit_group_quad_asm(u, out, cells=False, defer=False):
         out.append("            : " + ", ".join(outs))
         out.append('            : [qa] "v"(qa), [ka] "v"(ka), [kk] "v"(U.aku)')
         out.append('            : "memory");')
+        if cells:   # constrained cells: shapes past the allowed unpaired runs take no part
+            out.append("        if (U.mk) {")
+            out.append("            const int ml = %d - C.B, mh = C.A;" % u)
+            for u1 in ch:
+                out.append("            v%d = (%d >= ml && %d <= mh) ? v%d : INF16;" % (u1, u1, u1, u1))
+            out.append("        }")
         if ci_ == 0:
             if need_g:
                 out.append("        gk[0] = kr0.x; gk[1] = kr0.y; gk[2] = kr0.z; gk[3] = kr0.w; gk[4] = kr1.x; gk[5] = kr1.y;")
@@ -470,6 +476,14 @@ def sliced_parts(u, S, t):
     if u >= 2:
         lines.append("ds_read_b128 %%[kr1%s], %%[kk] offset:%d" % (t, 32 * u + 16))
         outs.append('[kr1%s] "=&v"(kr1%s)' % (t, t))
+    # constrained cells: shapes past the allowed unpaired runs (u1 > A or u2 > B) take no part
+    post.append("if (U.mk) {")
+    post.append("    const int ml = %d - C.B, mh = C.A, rr = int(C.rs >> 2);" % u)
+    for u1 in spec:
+        post.append("    %s = (%d >= ml && %d <= mh) ? %s : INF16;" % (V(u1), u1, u1, V(u1)))
+    for k in range(nk):
+        post.append("    w%d%s = (%d + rr >= ml && %d + rr <= mh) ? w%d%s : INF16;" % (k, t, gen[0] + S * k, gen[0] + S * k, k, t))
+    post.append("}")
     if gen:
         post.append("const uint32_t gk%s[6] = {kr0%s.x, kr0%s.y, kr0%s.z, kr0%s.w, kr1%s.x, kr1%s.y};" % ((t,) * 7))
     if u >= 2:
