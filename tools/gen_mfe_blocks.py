@@ -489,6 +489,7 @@ def sliced_parts(u, S, t):
     if u >= 2:
         post.append("const uint32_t fb%s = kr1%s.z, f1n%s = kr1%s.w;" % (t, t, t, t))
         post.append("(void)fb%s; (void)f1n%s;" % (t, t))
+    post.append("#ifndef MFE_ABL_SPEC")
     for u1 in spec:
         k = kind(u1, u - u1)
         v, c = V(u1), Cc(u1)
@@ -505,6 +506,8 @@ def sliced_parts(u, S, t):
             post.append("a.s = pmin(a.s, padd(%s, padd(padd(U.ct[CT_INVMM + %s], U.ct[CT_M23O + %s]), C.m23f)));" % (v, c, c))
         else:
             post.append("tv_%s = %s; ti_%s = U.ct[CT_INVMM + %s];" % (k, v, k, c))
+    post.append("#endif")
+    post.append("#ifndef MFE_ABL_GEN")
     pl = []
     for k in range(nk):
         vals = []
@@ -523,6 +526,7 @@ def sliced_parts(u, S, t):
         post.append("a.g%d = pmin(a.g%d, padd(w%d%s, %s));" % (k & 1, k & 1, k, t, e))
     if pl:
         post.extend(x.strip() for x in plateau_min(pl, "gk%s[%d]" % (t, KSAT), "    "))
+    post.append("#endif")
     return pre, decl, lines, outs, ins, post
 
 
@@ -535,12 +539,25 @@ def emit_sliced_batch(groups, S, out, ind):
     lines = sum((p[2] for p in parts), []) + ["s_waitcnt lgkmcnt(0)"]
     outs = sum((p[3] for p in parts), [])
     ins = sum((p[4] for p in parts), []) + ['[kk] "v"(U.aku)']
+    out.append("#ifndef MFE_ABL_READS")
     out.append(ind + "    asm volatile(")
     for ln in lines:
         out.append(ind + '        "%s\\n"' % ln)
     out.append(ind + "        : " + ", ".join(outs))
     out.append(ind + "        : " + ", ".join(ins))
     out.append(ind + '        : "memory");')
+    out.append("#else   // timing only: the batch's registers from VALU moves, no LDS")
+    out.append(ind + "    asm volatile(")
+    for ln in lines[:-1]:
+        reg = ln.split("%[")[1].split("]")[0]
+        if ln.startswith("ds_read_b128"):
+            continue   # left as is (garbage energies: timing only)
+        else:
+            out.append(ind + '        "v_mov_b32 %%[%s], 0\\n"' % reg)
+    out.append(ind + "        : " + ", ".join(outs))
+    out.append(ind + "        : " + ", ".join(ins))
+    out.append(ind + '        : "memory");')
+    out.append("#endif")
     for p in parts:
         out.extend(ind + "    " + x for x in p[5])
     out.append(ind + "}")
