@@ -1,7 +1,7 @@
 set -e
-mkdir -p gpurun_out/c20
+mkdir -p gpurun_out/c23
 export TMPDIR=/tmp ADX_MFE_KERNEL=cells
-timeout -k 10 300 python -u -m pytest tests/test_gpu_mfe.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/c20/pytest_mfe.log 2>&1
-timeout -k 10 120 python tools/pf_latency.py --fold mfe > gpurun_out/c20/lat.txt 2>&1
-ADX_NWV=8 ADX_LIB=addapt_amd/_lib/ablate/lib_s1.so timeout -k 10 120 python tools/cells_stamps.py 100 4096 > gpurun_out/c20/st4096.txt 2>&1
-timeout -k 10 300 python bench.py --steps 10 --no-cpu-baseline > gpurun_out/c20/bench.json 2> gpurun_out/c20/bench.err
+timeout -k 10 300 python -u -m pytest tests/test_gpu_mfe.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/c23/pytest_mfe.log 2>&1
+timeout -k 10 120 python tools/pf_latency.py --fold mfe > gpurun_out/c23/lat.txt 2>&1
+ADX_NWV=8 ADX_LIB=addapt_amd/_lib/ablate/lib_s1.so timeout -k 10 120 python tools/cells_stamps.py 100 4096 > gpurun_out/c23/st4096.txt 2>&1
+timeout -k 10 300 python bench.py --steps 10 --no-cpu-baseline > gpurun_out/c23/bench.json 2> gpurun_out/c23/bench.err
