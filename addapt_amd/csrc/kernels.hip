@@ -496,6 +496,9 @@ __device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
     out[3] = min(rc.cq, 4 * clampi(cdiv(hi - b2 * NW, rc.cb * NW), 0, rc.cqg));
 }
 
+#ifndef ADX_PRIO_Q5   // s_setprio of the q5 wave (0: off)
+#define ADX_PRIO_Q5 0
+#endif
 // ---------------------------------------------------------------- inside PF
 // P variants of one (context, macrostate) folded in lockstep (same cells,
 // same pairable set, same factors; the holo variant adds the motif bonus).
@@ -1086,6 +1089,9 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         // ---------------- q5[d] (the last wave: q5 is last in the cost order)
 #ifndef ADX_ABL_Q5
         if (wid == NW - 1 && (!incr || d >= m_lo - 1)) {   // q5[j < m_lo - 1] is unchanged
+#if ADX_PRIO_Q5
+            __builtin_amdgcn_s_setprio(ADX_PRIO_Q5);   // one-wave chain of the step
+#endif
 #else
         if (false) {
 #endif
@@ -1114,6 +1120,9 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                     L.q5[p][j] = SR::add((L.up[j] >= 1) ? SR::mul(L.q5[p][j - 1], sig1) : SR::zero(), sum[p]);
             }
         }
+#if ADX_PRIO_Q5
+        __builtin_amdgcn_s_setprio(0);
+#endif
         STAMP(6);
         if (has1 && m1np && i1 >= clo(d) && i1 <= chi(d)) {
 #pragma unroll
