@@ -263,3 +263,47 @@ def test_mc_mfe_full_size_incremental_consistency(native, oracle):
     sc, _, _ = eng.score_batch(final)
     for w in range(W):
         assert _close(scores[w], sc[w]), (w, scores[w], sc[w])
+
+
+def _par_with_mlbase(tmp_path, mlbase):
+    """The default parameter file with the multiloop unpaired-base energy cu set
+    (Turner 2004 has 0, which the kernel's qm1 column minima rely on; any other
+    value takes the direct unpaired loop)."""
+    src = workloads_par()
+    lines = open(src).read().split("\n")
+    k = lines.index("# ML_params")
+    while not lines[k].strip() or not lines[k].strip()[0].isdigit() and not lines[k].strip().startswith("-"):
+        k += 1
+    vals = lines[k].split()
+    vals[0] = str(mlbase)
+    lines[k] = "   " + "   ".join(vals)
+    out = tmp_path / "mlbase.par"
+    out.write_text("\n".join(lines))
+    return str(out)
+
+
+def workloads_par():
+    import os
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "addapt_amd", "data", "rna_turner2004_addapt.par")
+
+
+def test_fold_mfe_nonzero_mlbase(native, oracle, tmp_path):
+    """A parameter set with MLbase != 0 folds through the direct unpaired-run
+    loop of the qm rows (not the column minima) and stays bit-exact."""
+    path = _par_with_mlbase(tmp_path, 30)
+    P, OP = native.Params(path), oracle.Params(path)
+    rng = random.Random(23)
+    for n in (40, 100, 150):
+        for _ in range(3):
+            s = rand_seq(rng, n)
+            for cst in (None, rand_constraint(rng, n)):
+                f = native.Fold(s, params=P)
+                if cst:
+                    f.add_constraint(cst)
+                g = f.mfe()
+                ref = oracle.mfe_energy(s, cst, params=OP)
+                assert _same(g, ref), (s, cst, g, ref)
+    # and the default (MLbase = 0) parameters give a different answer somewhere
+    s = rand_seq(rng, 100)
+    assert oracle.mfe_energy(s, params=OP) >= oracle.mfe_energy(s)
