@@ -545,7 +545,7 @@ __device__ __forceinline__ void mfq_fold(const KArgs &ka, const DevScaled *__res
             const int j = i + d;
             const uint2 q0 = L.qbm[off(d, N) + i - 1];
             const bool pr = valid && (q0.x != MARK16 || q0.y != MARK16);
-            if (ls < Lb && pr) {   // only pairable cells' lanes (LDS cost ~ active lanes)
+            if (ls < Lb && pr) {   // only pairable cells' lanes (fewer lanes in bank-conflicting reads)
                 const int umax = d - 6 < 30 ? d - 6 : 30;
                 U.d = d;
                 U.umax = umax;

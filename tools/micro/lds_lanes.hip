@@ -1,6 +1,9 @@
-// Microbenchmark: does a ds_read_b32 wave-instruction cost fewer LDS cycles when
-// a 32-lane group has no active lane?  Each wave issues R rounds of 16 reads with
-// `active` lanes enabled; prints ms per variant.  (diagnostic, not product code)
+// Microbenchmark: LDS time of ds_read_b32 against the number of active lanes.
+// Each wave issues R rounds of 16 reads with `active` lanes enabled; prints ms per
+// variant.  Note the addresses: lane stride 8 words puts every 4th lane on one
+// bank, so this measures a bank-conflicted pattern (time ~ active lanes); a
+// conflict-free read costs one LDS cycle per 32-lane group whatever the lanes.
+// (diagnostic, not product code)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
