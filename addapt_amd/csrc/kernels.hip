@@ -2009,12 +2009,14 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
     for (int s = 0; s < st.nsteps; s++) {
         hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
+        // the event window covers the outside pass too when the terms read base-pair
+        // probabilities (bench.py divides bppm + score work by it)
+        if (evs) (void)hipEventRecord(evs[2 * s], stream);
         if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
             hipError_t e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0,
                                        const_cast<double *>(ka.pair_p), ka.bppm_scratch, stream);
             if (e != hipSuccess) return e;
         }
-        if (evs) (void)hipEventRecord(evs[2 * s], stream);
         hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);
         if (e != hipSuccess) return e;

@@ -118,3 +118,20 @@ def outside_flops(seq, cst=None):
             j = i + d
             ml += 2 * max(0, N - j - 4) + 4 * (i - 1)
     return 3 * a + ml
+
+
+# gfx950 VALU peaks (MI355X_MICROARCH.md: 256 CUs, 2.4 GHz, 4 SIMDs x 16 lanes = 64
+# lane-ops per clock per CU for a 32-bit VALU op)
+CUS, CLOCK_HZ, LANE_OPS_PER_CLK = 256, 2.4e9, 64
+
+
+def valu_peak(fold):
+    """(peak, note) in TFLOP/s (pf) or Top/s (mfe) for the work bench.py counts."""
+    if fold == "pf":
+        return 157.3, ("fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
+                       "products, not a contraction); peak = gfx950 fp32 vector rate (packed FMA), "
+                       "157.3 TFLOP/s")
+    peak = CUS * CLOCK_HZ * LANE_OPS_PER_CLK * 2 / 1e12
+    return peak, ("packed int16 VALU (v_pk_add_i16 / v_pk_min_i16 on apo|holo halves; min-plus is "
+                  "not an MFMA contraction); peak = 256 CUs x 64 lanes x 2 halves x 2.4 GHz = "
+                  "%.1f Top/s" % peak)

@@ -15,9 +15,13 @@ reference's own scoring path; config 3 without the bppm term).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 4096] [--length 100] [--fold mfe|pf]
 
-N > 1: launched by torch.distributed.run, one rank per GPU; walkers are
-sharded (weak scaling, global walker id = rank * W + w), no collective on
-the data path; a barrier + max-over-ranks brackets the timed region.
+N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) each
+process is one rank; a plain `python bench.py --gpus N` starts that launcher
+itself as a child process before anything touches the GPU (N larger than the
+visible GPU count is refused with exit status 2).  Walkers are sharded (weak
+scaling, global walker id = rank * W + w), no collective on the data path; a
+barrier + max-over-ranks brackets the timed region.  `--dry-run` replaces the
+engine by a host sleep over gloo (CPU-only test of the launch path).
 """
 import argparse
 import json
@@ -30,15 +34,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MC steps/sec (fold+score+accept), 100-nt sgRNA, 4096 walkers, 1/8 GPU"
-FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix rate
 HBM_PEAK_GBPS = 8000.0
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=300,
+                    help="timed steps (default: one annealing cycle of the 5 -> 0 in 300 schedule)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--walkers", type=int, default=4096)
     ap.add_argument("--length", type=int, default=100)
     ap.add_argument("--fold", choices=("mfe", "pf"), default="mfe",
@@ -54,7 +58,61 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic "
                          "(default profiles/traffic_latest_<fold>.json)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks, a host sleep per step (tests the --gpus N launch path)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` without a launcher: start torch.distributed.run as a
+    child (nothing here has touched the GPU: device_count() does not initialise
+    it) and return its exit status."""
+    import subprocess
+
+    if not a.dry_run:
+        import torch
+
+        visible = torch.cuda.device_count()
+        if a.gpus > visible:
+            print("bench.py: --gpus %d but %d GPU(s) visible" % (a.gpus, visible), file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def host_cores():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota
+    (a GPU box shares its host; nproc shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"usable": min(n, quota) if quota else n, "nproc": os.cpu_count(), "affinity": n,
+            "cgroup_quota": quota, "cpu_model": model}
 
 
 def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
@@ -62,7 +120,8 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
     from oracle import oracle as O
     from addapt_amd import workloads
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    hc = host_cores()
+    threads = hc["usable"]
     motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
     sf = O.ScoreFunction(terms, aptamer=motif, mode=fold)
     th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
@@ -82,6 +141,7 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
                       % (walkers, steps, "ViennaRNA-style pf, FP64" if fold == "pf"
                          else "integer-dcal MFE", t),
             "per_core": total / t / threads,
+            "nproc": hc["nproc"], "cgroup_quota": hc["cgroup_quota"], "cpu_model": hc["cpu_model"],
             "reference_2016_per_core": 14.4}
 
 
@@ -93,11 +153,42 @@ def mfe_kernel_label():
         k, "mfe_cells_kernel (lanes = cells, 2 folds per cell)") + " + FP32 MinPlus fallback launch"
 
 
+def dry_run(a, rank, world):
+    """CPU-only rehearsal of the rank launch: gloo barrier, a sleep per step, max over ranks."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    from addapt_amd import shard
+
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.001 * a.steps * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": a.walkers * a.steps * world / elapsed,
+                          "unit": "MC steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": elapsed / a.steps * 1e3, "dry_run": True,
+                          "ranks": shard.walker_ids(rank, world, a.walkers)[:1]}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    if a.dry_run:
+        return dry_run(a, rank, world)
     dist = None
     if world > 1:
         import torch
@@ -182,19 +273,17 @@ def main():
             tj = json.load(f)
         traffic = tj.get("bytes_per_launch")
         traffic_src = os.path.relpath(a.traffic_json, ROOT)
+    peak, peak_note = roofline.valu_peak(a.fold)
     roof = {
-        "bound": "mfma",
+        "bound": "valu",
         "achieved": achieved_tflops,
-        "peak": FP32_PEAK_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": (achieved_tflops / FP32_PEAK_TFLOPS) if achieved_tflops else None,
+        "peak": peak,
+        "unit": "TFLOP/s" if a.fold == "pf" else "Top/s",
+        "frac": (achieved_tflops / peak) if achieved_tflops else None,
         "traffic": traffic,
-        "compute_unit": ("fp32 VALU (no MFMA: the McCaskill recurrence is a sum of data-dependent "
-                         "products, not a contraction); peak = gfx950 fp32 rate, vector == matrix")
-        if a.fold == "pf" else
-        ("fp32 VALU add/min on integer dcal energies (min-plus is not an MFMA contraction); "
-         "peak = gfx950 fp32 rate"),
-        "kernel": mfe_kernel_label() if a.fold == "mfe" else "score_kernel<SumProd>",
+        "compute_unit": peak_note,
+        "kernel": ("bppm_kernel + score_kernel<SumProd> (one event window per step)" if a.bppm
+                   else mfe_kernel_label() if a.fold == "mfe" else "score_kernel<SumProd>"),
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": score_ms,
         "launches": launches,
@@ -207,6 +296,7 @@ def main():
         # incremental refold (read back for the unchanged cells, <= the same again)
         "algorithmic_bytes_per_launch": (scored / max(1, a.steps)) * (a.length + 8 + 2 * state_bytes),
         "state_bytes_per_scored_walker": state_bytes,
+        "hbm_peak_GBps": HBM_PEAK_GBPS,
     }
     out = {
         "metric": METRIC,
@@ -219,7 +309,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",   # MFE: integer dcal/mol values, exact in fp32 add/min
+        # MFE: integer dcal/mol, apo|holo as two int16 halves of one 32-bit word
+        # (v_pk_add_i16 / v_pk_min_i16); PF: fp32 Boltzmann factors
+        "dtype": "i16x2" if a.fold == "mfe" else "fp32",
         "data": "synthetic",
         "config": {
             "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
