@@ -120,9 +120,10 @@ def outside_flops(seq, cst=None):
     return 3 * a + ml
 
 
-# gfx950 VALU peaks (MI355X_MICROARCH.md: 256 CUs, 2.4 GHz, 4 SIMDs x 16 lanes = 64
-# lane-ops per clock per CU for a 32-bit VALU op)
-CUS, CLOCK_HZ, LANE_OPS_PER_CLK = 256, 2.4e9, 64
+# gfx950 VALU peaks (MI355X_MICROARCH.md: 256 CUs, 2.4 GHz).
+# 4 SIMD-32 per CU, a wave64 VALU instruction in 2 cycles (MI355X_MICROARCH.md):
+# 128 lane-instructions per clock per CU
+CUS, CLOCK_HZ, LANE_OPS_PER_CLK = 256, 2.4e9, 128
 
 
 def valu_peak(fold):
@@ -133,5 +134,5 @@ def valu_peak(fold):
                        "157.3 TFLOP/s")
     peak = CUS * CLOCK_HZ * LANE_OPS_PER_CLK * 2 / 1e12
     return peak, ("packed int16 VALU (v_pk_add_i16 / v_pk_min_i16 on apo|holo halves; min-plus is "
-                  "not an MFMA contraction); peak = 256 CUs x 64 lanes x 2 halves x 2.4 GHz = "
+                  "not an MFMA contraction); peak = 256 CUs x 128 lanes/clk x 2 halves x 2.4 GHz = "
                   "%.1f Top/s" % peak)
