@@ -10,12 +10,14 @@ accepted with probability
 
     min(1, exp((S(y) - S(x)) * (1/T_lo - 1/T_hi))).
 
-Both ranks of a pair draw the same uniforms (a generator keyed by the run
-seed, the round and the pair), so the decision needs no extra message; the
-one exchange per round is the pair's full configuration arrays, W*(N + 8)
-bytes each way, sent point to point over RCCL (xGMI) from device buffers the
-engine exports (adx_walkers_export / adx_walkers_import).  RNG streams,
-counters and thermostat state stay with the walker slot.
+Both ranks of a pair draw the same uniforms (a generator on the device keyed
+by the run seed, the round and the pair), so the decision needs no extra
+message; the one exchange per round is the pair's configurations packed into
+a single W*(N + 8)-byte buffer each way, sent point to point over RCCL (xGMI)
+from device buffers the engine exports (adx_walkers_export /
+adx_walkers_import), and the accept mask and the swap are computed on the
+device.  RNG streams, counters and thermostat state stay with the walker
+slot.
 """
 import math
 
@@ -35,53 +37,81 @@ def partner(rank, world, round_idx):
     return p if 0 <= p < world else None
 
 
+def _key(seed, round_idx, lo_rank):
+    """63-bit generator key shared by both ranks of a pair."""
+    k = 0x9E3779B97F4A7C15
+    for x in (int(seed), int(round_idx), int(lo_rank)):
+        k = ((k ^ (x & 0xFFFFFFFFFFFFFFFF)) * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return k >> 1
+
+
+def swap_mask(seed, round_idx, lo_rank, s_lo, s_hi, t_lo, t_hi):
+    """Boolean mask over walker slots (a tensor on the scores' device): swap slot
+    w between rungs lo and hi.  The uniforms come from a generator on that
+    device keyed by (seed, round, lower rank), so both ranks of a pair -- on the
+    same kind of device -- take the same decisions without a message and
+    without a host round trip."""
+    import torch
+
+    g = torch.Generator(device=s_lo.device)
+    g.manual_seed(_key(seed, round_idx, lo_rank))
+    u = torch.rand(s_lo.shape, generator=g, device=s_lo.device, dtype=torch.float64)
+    a = (s_hi - s_lo) * (1.0 / t_lo - 1.0 / t_hi)
+    acc = (a >= 0) | (torch.log(u) < a)          # NaN a (inf - inf) compares false
+    return acc & torch.isfinite(s_lo) & torch.isfinite(s_hi)
+
+
 def swap_accept(seed, round_idx, lo_rank, s_lo, s_hi, t_lo, t_hi):
-    """Boolean mask over walker slots: swap slot w between rungs lo and hi."""
-    s_lo = np.asarray(s_lo, dtype=np.float64)
-    s_hi = np.asarray(s_hi, dtype=np.float64)
-    rng = np.random.Generator(np.random.PCG64([int(seed), int(round_idx), int(lo_rank)]))
-    u = rng.random(s_lo.shape[0])
-    with np.errstate(invalid="ignore", over="ignore"):
-        a = (s_hi - s_lo) * (1.0 / t_lo - 1.0 / t_hi)
-        acc = (a >= 0) | (np.log(u) < a)
-    return acc & np.isfinite(s_lo) & np.isfinite(s_hi)
+    """swap_mask on host arrays (CPU generator), as a numpy bool array."""
+    import torch
+
+    m = swap_mask(seed, round_idx, lo_rank, torch.as_tensor(np.asarray(s_lo, dtype=np.float64)),
+                  torch.as_tensor(np.asarray(s_hi, dtype=np.float64)), t_lo, t_hi)
+    return m.numpy()
 
 
 def exchange_round(dist, round_idx, rank, world, temps, seqs, scores, seed=0):
     """One exchange round on this rank.  seqs (uint8 [W, N]) and scores
     (float64 [W]) are torch tensors on the communication device (CUDA for
-    RCCL, CPU for gloo), updated in place.  Returns (attempted, accepted)."""
+    RCCL, CPU for gloo), updated in place.  The pair's configurations travel
+    as ONE packed [W, N + 8] byte buffer each way (one send + one receive,
+    device to device over RCCL/xGMI); the decision and the swap stay on the
+    device.  Returns (attempted, accepted) as device tensors' values."""
     import torch
 
     p = partner(rank, world, round_idx)
     if p is None:
         return 0, 0
-    # RCCL moves the device buffers directly; gloo (CPU tests) needs host copies
-    host = dist.get_backend() == "gloo" and seqs.is_cuda
-    snd_seqs, snd_scores = (seqs.cpu(), scores.cpu()) if host else (seqs, scores)
-    other_seqs = torch.empty_like(snd_seqs)
-    other_scores = torch.empty_like(snd_scores)
-    ops = [dist.P2POp(dist.isend, snd_seqs, p), dist.P2POp(dist.isend, snd_scores, p),
-           dist.P2POp(dist.irecv, other_seqs, p), dist.P2POp(dist.irecv, other_scores, p)]
+    W, N = seqs.shape
+    packed = torch.cat([seqs, scores.view(torch.uint8).reshape(W, 8)], dim=1).contiguous()
+    # gloo (CPU tests) moves host tensors only
+    host = dist.get_backend() == "gloo" and packed.is_cuda
+    snd = packed.cpu() if host else packed
+    rcv = torch.empty_like(snd)
+    ops = [dist.P2POp(dist.isend, snd, p), dist.P2POp(dist.irecv, rcv, p)]
     for req in dist.batch_isend_irecv(ops):
         req.wait()
     if host:
-        other_seqs, other_scores = other_seqs.to(seqs.device), other_scores.to(seqs.device)
+        rcv = rcv.to(seqs.device)
+    other_seqs = rcv[:, :N]
+    other_scores = rcv[:, N:].contiguous().view(torch.float64).reshape(W)
     lo, hi = min(rank, p), max(rank, p)
-    mine = scores.cpu().numpy()
-    theirs = other_scores.cpu().numpy()
-    s_lo, s_hi = (mine, theirs) if rank == lo else (theirs, mine)
-    acc = swap_accept(seed, round_idx, lo, s_lo, s_hi, temps[lo], temps[hi])
-    if acc.any():
-        idx = torch.from_numpy(np.nonzero(acc)[0]).to(seqs.device)
-        seqs[idx] = other_seqs[idx]
-        scores[idx] = other_scores[idx]
-    return int(acc.size), int(acc.sum())
+    s_lo, s_hi = (scores, other_scores) if rank == lo else (other_scores, scores)
+    # both ranks of the pair draw on the same kind of device: the CPU generator
+    # under gloo, the device generator under RCCL
+    dev_scores = s_lo if not host else s_lo.cpu()
+    acc = swap_mask(seed, round_idx, lo, dev_scores, s_hi if not host else s_hi.cpu(),
+                    temps[lo], temps[hi]).to(seqs.device)
+    seqs.copy_(torch.where(acc[:, None], other_seqs, seqs))
+    scores.copy_(torch.where(acc, other_scores, scores))
+    return int(acc.numel()), int(acc.sum())
 
 
-def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda"):
+def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda", observe=None):
     """Advance `engine` (a native.Engine of this rank, fixed thermostat) by
-    `steps` MC steps with an exchange every `interval` steps."""
+    `steps` MC steps with an exchange every `interval` steps.  `observe`
+    (tests): called per round with host copies (round, seqs, scores before,
+    seqs, scores after the exchange)."""
     import torch
 
     engine.set_temperature(temps[rank])
@@ -95,7 +125,10 @@ def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda"
         done += k
         if done < steps or k == interval:
             engine.export_walkers(seqs.data_ptr(), scores.data_ptr())
+            before = (seqs.cpu().numpy().copy(), scores.cpu().numpy().copy()) if observe else None
             a, b = exchange_round(dist, rnd, rank, world, temps, seqs, scores, seed)
+            if observe:
+                observe(rnd, before[0], before[1], seqs.cpu().numpy().copy(), scores.cpu().numpy().copy())
             if seqs.is_cuda:
                 torch.cuda.synchronize()   # the engine copies on its own stream
             engine.import_walkers(seqs.data_ptr(), scores.data_ptr())

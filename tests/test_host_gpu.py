@@ -136,3 +136,60 @@ def test_cpp_base_pair_prob_matches_oracle(oracle, tmp_path, holo):
         assert abs(float(p) - ref[int(i), int(j)]) <= 2e-4, (i, j, p, ref[int(i), int(j)])
     sym = [l for l in lines if l.startswith("sym")][0]
     assert abs(float(sym.split()[1]) - ref[0, len(seq) - 1]) <= 2e-4
+
+
+def _closure(active, pos):
+    """Positions mutate_recursively touches from pos (sampling.cc:195-282)."""
+    st, pt = [], {}
+    for k, c in enumerate(active):
+        if c == "(":
+            st.append(k)
+        elif c == ")":
+            a = st.pop()
+            pt[a], pt[k] = k, a
+    seen, todo = {pos}, [pos]
+    while todo:
+        k = todo.pop()
+        if k in pt and pt[k] not in seen:
+            seen.add(pt[k])
+            todo.append(pt[k])
+    return seen
+
+
+@pytest.mark.gpu
+def test_config1_cli_10k_steps_matches_golden(tmp_path):
+    """BASELINE configs[0] end to end: the addapt CLI, rhf(6), default objective,
+    "5 to 0 in 300 steps", seed 0, 10 000 steps (apps/addapt.cc:58-103), against
+    the oracle's trajectory committed in tests/golden/config1_rhf6_seed0.json
+    (tests/golden/gen_config1.py): every step's move (position, base) and
+    outcome bit-exact.  The only admissible difference is a Metropolis near tie
+    that the FP32 fold decides the other way: |log crit - log u| of the oracle
+    below the fold's error bound at that temperature; the trajectories cannot
+    be compared past it, so it must come late."""
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "config1_rhf6_seed0.json")) as f:
+        g = json.load(f)
+    steps = g["steps"]
+    cfg = _config(tmp_path)
+    out = str(tmp_path / "traj.tsv")
+    _run([cfg, "-n", str(steps), "-r", "0", "-o", out], timeout=900)
+    _, rows = _read_tsv(out)
+    assert len(rows) == steps
+    prev = workloads.RHF6_SEQ
+    active = workloads.RHF6_ACTIVE
+    for s, r in enumerate(rows):
+        pos, base = g["pos"][s], g["base"][s]
+        prop = r["proposed_seq"]
+        moved = {k for k in range(len(prev)) if prop[k] != prev[k]}
+        same_move = prop[pos].upper() == base and moved <= _closure(active, pos)
+        same_outcome = OUTC[r["outcome"]] == int(g["outcome"][s])
+        if not (same_move and same_outcome):
+            m, T = g["margin"][s], float(r["temperature"])
+            # |d score| <= 2e-3 between the FP32 and FP64 folds (test_gpu_parity.py)
+            bound = 4e-3 / T if T > 0 else math.inf
+            assert same_move and m is not None and abs(m) <= bound and s >= 1000, \
+                (s, pos, base, r["outcome"], g["outcome"][s], m)
+            pytest.skip("near tie at step %d (margin %.2e <= %.2e): %d steps bit-exact" % (s, m, bound, s))
+        prev = r["current_seq"]
+    assert prev == g["final_seq"]

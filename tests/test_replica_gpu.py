@@ -3,6 +3,7 @@ configurations and a 2-rung ladder (2 processes on cuda:0, gloo for the
 exchange -- RCCL needs one GPU per rank; the 8-GPU node uses RCCL)."""
 import os
 import socket
+import zlib
 
 import numpy as np
 import pytest
@@ -91,3 +92,80 @@ def test_two_rung_ladder():
         assert err <= 2e-3          # imported scores still describe the imported sequences
         assert n == 16 * 20
     assert res[0][1]["attempted"] > 0
+
+
+def _rung_config5(rank, world, port, q):
+    """BASELINE configs[4] on one GPU: one rung per process, N = 100, 4096
+    walkers per rung, partition-function objective, 3 exchange rounds."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from addapt_amd import native, replica
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, N, steps, interval = 4096, 100, 15, 5
+        tmpl, active = workloads.synthetic(N)
+        apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+        temps = replica.ladder_temperatures(world)
+        eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt,
+                            thermostat=native.make_thermostat("fixed", t=temps[rank]))
+        ids = list(range(rank * W, (rank + 1) * W))
+        eng.walkers_init(ids, workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + ids[0]))
+        rounds = []
+
+        def observe(rnd, s0, sc0, s1, sc1):
+            # per round: which slots changed, and hashes of the configurations
+            changed = np.nonzero((s0 != s1).any(axis=1) | (sc0 != sc1))[0]
+            # deterministic across processes (Python's hash() is salted per process)
+            key = lambda s, sc: [zlib.crc32(bytes(s[w]) + sc[w].tobytes()) for w in range(W)]
+            rounds.append((rnd, key(s0, sc0), key(s1, sc1), changed.size))
+
+        stats = replica.run(eng, dist, rank, world, steps=steps, interval=interval, temps=temps,
+                            seed=11, observe=observe)
+        seqs, scores, counters = eng.download()
+        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+        sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
+        sample = list(range(0, W, W // 8))
+        err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in sample)
+        q.put((rank, stats, rounds, float(err), counters.sum(axis=0).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_config5_ladder_at_workload():
+    """Replica exchange at BASELINE configs[4]'s per-rung size (two rungs on one
+    GPU, gloo for the exchange): configurations are conserved by every exchange
+    round (slot by slot, the pair's two configurations are the same multiset
+    before and after), sampled walkers' scores match the oracle after the
+    exchanges, and every rung counts W x steps MC steps."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rung_config5, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=600)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    W = 4096
+    r0, r1 = res[0], res[1]
+    assert r0[1]["rounds"] == r1[1]["rounds"] == 3
+    exchanged = 0
+    for (a, b) in zip(r0[2], r1[2]):
+        rnd, before0, after0, _ = a
+        _, before1, after1, _ = b
+        for w in range(W):
+            assert sorted((before0[w], before1[w])) == sorted((after0[w], after1[w])), (rnd, w)
+        exchanged += sum(1 for w in range(W) if after0[w] != before0[w])
+    assert exchanged > 0
+    assert r0[1]["accepted"] == r1[1]["accepted"]   # both ranks took the same decisions
+    for rank in (0, 1):
+        assert res[rank][3] <= 2e-3, res[rank][3]
+        assert sum(res[rank][4]) == W * 15
