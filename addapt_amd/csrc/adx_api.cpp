@@ -141,7 +141,7 @@ void build_tables(const EnergyParams &P, DevTables &T, bool mfe) {
 struct Motif {
     std::string seq, fold;
     double energy_kcal = 0.0;
-    int mode = ADX_MOTIF_ADD;
+    int mode = ADX_MOTIF_AUTO;
     bool present = false;
 };
 
@@ -310,7 +310,8 @@ void build_scaled(const EnergyParams &P, double sigma, const Motif &m, double ei
             X.motif_code[k] = static_cast<uint8_t>(base_code(m.seq[k]));
             X.motif_pt[k] = static_cast<int8_t>(mpt[k]);
         }
-        const double beff = (m.mode == ADX_MOTIF_REPLACE) ? m.energy_kcal - eint : m.energy_kcal;
+        const bool replace = m.mode == ADX_MOTIF_REPLACE || (m.mode == ADX_MOTIF_AUTO && mfe);
+        const double beff = replace ? m.energy_kcal - eint : m.energy_kcal;
         if (mfe) {   // min-plus image of the extra term: the formed motif's energy, rounded once to dcal
             X.motif_extra = static_cast<float>(std::lround(100.0 * (eint + beff)));
         } else {

@@ -17,7 +17,7 @@ DEFAULT_PARAMS = os.path.join(HERE, "data", "rna_turner2004_addapt.par")
 OK, EINVAL, EHIP, ECONSTRAINT, EPARAM, ENOMEM, EMOVE, ESTATE, ENODEV, EUNSUPPORTED = range(10)
 APO, HOLO = 0, 1
 THERMO_FIXED, THERMO_ANNEAL, THERMO_AUTO = 0, 1, 2
-MOTIF_ADD, MOTIF_REPLACE = 0, 1
+MOTIF_ADD, MOTIF_REPLACE, MOTIF_AUTO = 0, 1, 2
 FOLD_PF, FOLD_MFE = 0, 1
 TERM_MACROSTATE, TERM_PAIR = 0, 1
 OUTCOMES = ["REJECT", "ACCEPT_WORSENED", "ACCEPT_UNCHANGED", "ACCEPT_IMPROVED"]
@@ -221,7 +221,7 @@ class Engine:
     """
 
     def __init__(self, sequence, macrostates, terms, aptamer=None, thermostat=None, contexts=None,
-                 motif_mode=MOTIF_ADD, params=None, device=0, fold_mode="pf"):
+                 motif_mode=MOTIF_AUTO, params=None, device=0, fold_mode="pf"):
         self.params = params or default_params()
         self.N = len(sequence)
         d = RunDesc()

@@ -122,7 +122,7 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
 
     hc = host_cores()
     threads = hc["usable"]
-    motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+    motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
     sf = O.ScoreFunction(terms, aptamer=motif, mode=fold)
     th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     # probe: 1 walker x 4 steps on one thread to size the sample

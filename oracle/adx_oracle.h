@@ -74,7 +74,9 @@ const char *orc_last_error(void);
 /* ---- folding ---------------------------------------------------------- */
 /* Ligand motif (vrna_sc_add_hi_motif, scoring.cc:92-100).  mode 0 = "add"
  * (bonus added to the motif structure's intrinsic energy), mode 1 =
- * "replace" (motif structure's total energy := bonus). */
+ * "replace" (motif structure's total energy := bonus), mode 2 = "auto"
+ * (add in partition functions, replace in the MFE: the conventions the
+ * reference's RNAfold annotations pin, test_scoring.cc:52-55 and :154). */
 typedef struct orc_motif {
     const char *seq;     /* upper case ACGU */
     const char *fold;    /* dot-bracket, outer pair spans the motif */

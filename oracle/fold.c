@@ -198,7 +198,7 @@ typedef struct {
     const char *mseq;
     double m_extra; /* Boltzmann extra weight for a formed motif (unscaled) */
     double m_Eint;
-    double m_beff;  /* bonus applied to the formed motif (kcal; mode REPLACE: minus Eint) */
+    double m_beff;  /* PF bonus applied to the formed motif (kcal; mode REPLACE: minus Eint) */
     int m_mfe_dcal; /* motif structure energy incl. bonus for the MFE, lround(100*(Eint+beff)) */
 } model_t;
 
@@ -257,10 +257,14 @@ static int model_init(model_t *m, const orc_params *P, const char *seq, const ch
         free(stk);
         double eint = orc_eval_structure(P, motif->seq, motif->fold); /* kcal */
         m->m_Eint = eint;
+        /* mode 2 (auto): ADD for partition functions, REPLACE for the MFE --
+         * the conventions the reference's two RNAfold annotations pin
+         * (ensemble dG test_scoring.cc:52-55, holo MFE test_scoring.cc:154) */
         double beff = motif->mode == 1 ? motif->energy_kcal - eint : motif->energy_kcal;
+        double beff_mfe = motif->mode == 0 ? motif->energy_kcal : motif->energy_kcal - eint;
         m->m_extra = boltz(eint * 100.0) * (boltz(beff * 100.0) - 1.0);
         m->m_beff = beff;
-        m->m_mfe_dcal = (int)lround(100.0 * (eint + beff));
+        m->m_mfe_dcal = (int)lround(100.0 * (eint + beff_mfe));
     }
     return 1;
 }

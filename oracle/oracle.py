@@ -149,7 +149,7 @@ def default_params():
     return _default_params
 
 
-def make_motif(seq, fold, energy_kcal, mode=0):
+def make_motif(seq, fold, energy_kcal, mode=2):
     m = Motif(_b(seq), _b(fold), energy_kcal, mode)
     m._keep = (seq, fold)
     return m

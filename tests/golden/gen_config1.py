@@ -27,7 +27,7 @@ from oracle import oracle as O  # noqa: E402
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-    motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+    motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
     sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
     th = O.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     r = O.mc_run(sf, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], th, 0, steps)

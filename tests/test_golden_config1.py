@@ -14,7 +14,7 @@ def test_golden_prefix_replays(oracle):
         g = json.load(f)
     assert g["steps"] == 10000 and len(g["pos"]) == len(g["base"]) == len(g["outcome"]) == 10000
     assert sum(g["counters"]) == 10000
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
     th = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     n = 120

@@ -48,7 +48,7 @@ def test_fold_bpp_motif(native, oracle):
     for seq in (apt, "GGGA" + apt + "UCCC"):
         f = native.Fold(seq)
         f.add_motif(apt, fold, e)
-        _, ref = oracle.bppm(seq, None, oracle.make_motif(apt, fold, e, 0))
+        _, ref = oracle.bppm(seq, None, oracle.make_motif(apt, fold, e))
         n = len(seq)
         got = np.array([[f.bpp(i + 1, j + 1) for j in range(n)] for i in range(n)])
         assert np.abs(got - ref).max() <= P_TOL, (seq, np.abs(got - ref).max())
@@ -67,7 +67,7 @@ def _engine(native, tmpl, macro, terms, thermostat=None, contexts=None):
 
 
 def _oracle_sf(oracle, terms, contexts=None):
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts)
 
 
@@ -76,7 +76,7 @@ def test_bppm_batch(native, oracle, N):
     tmpl, active = workloads.synthetic(N)
     eng = _engine(native, tmpl, [active], _objective(N))
     seqs = workloads.walker_sequences(tmpl, [active], 6)
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     for cond in ("apo", "holo"):
         got = eng.bppm_batch(seqs, cond)
         for w in range(6):

@@ -86,7 +86,7 @@ def test_score_batch_mfe_mixed_fallback(native, oracle):
                 s[i] = "G" if i < 75 else "C"
         seqs[w] = "".join(s)
     sc, tv, dg = eng.score_batch(seqs)
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     for v in range(eng.info.n_variants):
         _, cond, mac = eng.variant(v)
         for w in range(8):
@@ -98,7 +98,7 @@ def test_fold_mfe_motif(native, oracle):
     apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
     e = oracle.theo_bonus()
     rng = random.Random(5)
-    m = oracle.make_motif(apt, fold, e, 0)
+    m = oracle.make_motif(apt, fold, e)
     for seq in (apt, "GGGA" + apt + "UCCC", rand_seq(rng, 20) + apt + rand_seq(rng, 31),
                 workloads.synthetic(100)[0].upper()):
         for cst in (None, "." * len(seq)):
@@ -117,7 +117,7 @@ def _engine(native, tmpl, macro, terms, thermostat=None, contexts=None):
 
 
 def _oracle_sf(oracle, terms, contexts=None):
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts, mode="mfe")
 
 
@@ -134,7 +134,7 @@ def test_score_batch_mfe(native, oracle, N):
     eng = _engine(native, tmpl, [active], terms)
     seqs = workloads.walker_sequences(tmpl, [active], 24)
     sc, tv, dg = eng.score_batch(seqs)
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     for v in range(eng.info.n_variants):
         _, cond, mac = eng.variant(v)
         for w in range(24):
@@ -227,7 +227,7 @@ def test_mc_trajectory_contexts_incremental(native, oracle, fold):
     eng.walkers_init(seeds, seqs)
     tr = eng.run_steps(steps, trace=True)
     final, scores, counters = eng.download()
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     sf = oracle.ScoreFunction(terms, aptamer=m, contexts=ctx, mode=fold)
     therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
     tie = 1e-12 if fold == "mfe" else 1e-6

@@ -67,7 +67,7 @@ def test_fold_layer_motif(native, oracle):
             if cst:
                 f.add_constraint(cst)
             g = f.pf()
-            ref = oracle.pf_energy(seq, cst, oracle.make_motif(apt, fold, e, 0))
+            ref = oracle.pf_energy(seq, cst, oracle.make_motif(apt, fold, e))
             assert abs(g - np.float32(ref)) <= DG_TOL, (seq, g, ref)
 
 
@@ -78,7 +78,7 @@ def _engine(native, tmpl, macro, terms, aptamer=True, contexts=None, thermostat=
 
 
 def _oracle_sf(oracle, terms, aptamer=True, contexts=None):
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0) if aptamer else None
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus()) if aptamer else None
     return oracle.ScoreFunction(terms, aptamer=m, contexts=contexts)
 
 
@@ -89,7 +89,7 @@ def test_score_batch_synthetic(native, oracle, N):
     eng = _engine(native, tmpl, [active], terms)
     seqs = workloads.walker_sequences(tmpl, [active], 16)
     sc, tv, dg = eng.score_batch(seqs)
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     for v in range(eng.info.n_variants):
         _, cond, mac = eng.variant(v)
         for w in (0, 5, 15):

@@ -61,7 +61,7 @@ def test_cli_trajectory_matches_oracle(oracle, tmp_path):
     assert len(rows) == steps
     assert "term_value[apo: not active]" in head and "term_value[holo: active]" in head
     outc = [OUTC[r["outcome"]] for r in rows]
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
     th = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
     ref = oracle.mc_run(sf, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], th, 0, steps, forced=outc,
@@ -99,7 +99,7 @@ def test_cli_batched_walkers(oracle, tmp_path):
     _run([cfg, "-n", str(steps), "-r", "100", "--walkers", str(W), "-o", out])
     lines = open(out).read().splitlines()
     assert len(lines) == W + 1
-    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
     for l in lines[1:]:
         f = l.split("\t")
@@ -126,7 +126,7 @@ def test_cpp_base_pair_prob_matches_oracle(oracle, tmp_path, holo):
     r = subprocess.run([exe, seq] + (["holo"] if holo else []), stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0) if holo else None
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus()) if holo else None
     _, ref = oracle.bppm(seq, None, m)
     lines = r.stdout.split("\n")
     for line in lines:

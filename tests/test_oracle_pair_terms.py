@@ -12,7 +12,7 @@ from addapt_amd import workloads
 def test_pair_term_value(oracle):
     tmpl, active = workloads.synthetic(60)
     seq = workloads.walker_sequences(tmpl, [active], 1)[0]
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
     terms = [("apo", ("pair", 0, 59), False, 1.0), ("holo", ("pair", 1, 58), True, 2.0)]
     sf = oracle.ScoreFunction(terms, aptamer=m)
     s, tv = sf.score(seq, [active])

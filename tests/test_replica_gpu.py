@@ -67,7 +67,7 @@ def _rung(rank, world, port, q):
         stats = replica.run(eng, dist, rank, world, steps=20, interval=5,
                             temps=replica.ladder_temperatures(world), seed=3)
         seqs, scores, counters = eng.download()
-        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
         sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
         err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in range(W))
         q.put((rank, stats, float(err), int(counters.sum())))
@@ -125,7 +125,7 @@ def _rung_config5(rank, world, port, q):
         stats = replica.run(eng, dist, rank, world, steps=steps, interval=interval, temps=temps,
                             seed=11, observe=observe)
         seqs, scores, counters = eng.download()
-        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 0)
+        motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
         sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
         sample = list(range(0, W, W // 8))
         err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in sample)
