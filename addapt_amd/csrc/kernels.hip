@@ -496,9 +496,6 @@ __device__ inline void wave_range(const RangeCost &rc, int w, int (&out)[4]) {
     out[3] = min(rc.cq, 4 * clampi(cdiv(hi - b2 * NW, rc.cb * NW), 0, rc.cqg));
 }
 
-#ifndef ADX_PRIO_Q5   // s_setprio of the q5 wave (0: off)
-#define ADX_PRIO_Q5 0
-#endif
 // ---------------------------------------------------------------- inside PF
 // P variants of one (context, macrostate) folded in lockstep (same cells,
 // same pairable set, same factors; the holo variant adds the motif bonus).
@@ -992,11 +989,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 float A[P], Pp[P];
 #pragma unroll
                 for (int p = 0; p < P; p++) { A[p] = SR::zero(); Pp[p] = SR::zero(); }
-                int it = 0;
-#ifdef ADX_ABL_QM
-                it = nit;
-#endif
-                for (; it < nit; it++) {
+                for (int it = 0; it < nit; it++) {
                     const int t0 = it * 16 + l16;
                     const bool ok0 = cell && t0 <= tmax;
                     const bool okr = ok0 && t0 >= 5;
@@ -1048,13 +1041,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                 const bool masked = constrained && (u.A < umax || u.B < umax);
                 // gather of the prefetched 1x1..2x2 table factors for this cell
                 const float gtab = __shfl(pfx, c * 4 + D.gsel, WAVE);
-#ifndef ADX_ABL_QBT
                 if (masked) qb_terms_dispatch<SR, true, P>(sS, sG, L, D, u, gtab, part);
                 else qb_terms_dispatch<SR, false, P>(sS, sG, L, D, u, gtab, part);
-#else
-#pragma unroll
-                for (int p = 0; p < P; p++) part[p] = SR::mul(gtab, SR::zero());
-#endif
             };
             int c = 0;
             if constexpr (P == 1) {
@@ -1087,14 +1075,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         STAMP(4);
 
         // ---------------- q5[d] (the last wave: q5 is last in the cost order)
-#ifndef ADX_ABL_Q5
         if (wid == NW - 1 && (!incr || d >= m_lo - 1)) {   // q5[j < m_lo - 1] is unchanged
-#if ADX_PRIO_Q5
-            __builtin_amdgcn_s_setprio(ADX_PRIO_Q5);   // one-wave chain of the step
-#endif
-#else
-        if (false) {
-#endif
             const int j = d;
             const int sjp = (j < N) ? L.S[j + 1] : 5;
             const int sj = L.S[j];
@@ -1120,9 +1101,6 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
                     L.q5[p][j] = SR::add((L.up[j] >= 1) ? SR::mul(L.q5[p][j - 1], sig1) : SR::zero(), sum[p]);
             }
         }
-#if ADX_PRIO_Q5
-        __builtin_amdgcn_s_setprio(0);
-#endif
         STAMP(6);
         if (has1 && m1np && i1 >= clo(d) && i1 <= chi(d)) {
 #pragma unroll
@@ -1846,9 +1824,6 @@ static size_t lds_size(const KArgs &ka, int pl, bool rt) {
 }
 
 static int choose_p(const KArgs &ka) {
-#ifdef ADX_FORCE_P1
-    return 1;
-#endif
     return lds_size<2>(ka, 0, false) <= size_t(LDS_LIMIT) ? 2 : 1;
 }
 
@@ -1856,18 +1831,10 @@ static int choose_p(const KArgs &ka) {
 template <int P, int NT = (P == 2 ? ADX_NT2 : 512)>
 static void choose_opt(const KArgs &ka, int &pl, bool &rt) {
     // P = 1 keeps two workgroups per CU when they fit (1 KiB margin for allocation granularity)
-#ifdef ADX_1WG
-    const size_t lim = LDS_LIMIT;
-#else
     const size_t lim = (P == 1 && 2 * lds_size<1, NT>(ka, 0, false) <= size_t(LDS_LIMIT) - 2048)
                            ? LDS_LIMIT / 2 - 1024 : LDS_LIMIT;
-#endif
     rt = lds_size<P, NT>(ka, 0, true) <= lim;
     pl = lds_size<P, NT>(ka, 2, rt) <= lim ? 2 : lds_size<P, NT>(ka, 1, rt) <= lim ? 1 : 0;
-#ifdef ADX_NO_OPT
-    pl = 0;
-    rt = false;
-#endif
 }
 
 size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
@@ -1906,22 +1873,14 @@ size_t mfe_cells_lds(const KArgs &ka);
 hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
                             const int *mask, hipStream_t stream);
 
-size_t mfe_quad_lds(const KArgs &ka);
-hipError_t launch_mfe_quad(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
-                           const int *mask, hipStream_t stream);
-
-// MFE kernel choice, ADX_MFE_KERNEL: cells (default) = mfe_cells_kernel (lanes =
-// cells, two folds per cell, two walkers per CU); quad = mfe_quad_kernel (lanes =
-// cells, four folds per cell, one walker per CU: lower latency per walker, lower
-// throughput at 4096 walkers); rows = score_kernel<MinPlus16> (lanes = terms)
-static int mfe_kernel_choice() {
-    static const int v = [] {
-        const char *e = std::getenv("ADX_MFE_KERNEL");
-        if (e && std::strcmp(e, "rows") == 0) return 0;
-        if (e && std::strcmp(e, "quad") == 0) return 2;
-        return 1;
-    }();
-    return v;
+// MFE kernel choice, ADX_MFE_KERNEL (read at every launch, so a test can
+// switch it between contexts): cells (default) = mfe_cells_kernel (lanes =
+// cells, two folds per cell, two walkers per CU); rows = score_kernel<MinPlus16>
+// (lanes = terms) -- also the kernel for energy models or lengths the cells
+// kernel does not cover (mfe_cells_lds() == 0)
+static bool mfe_rows_forced() {
+    const char *e = std::getenv("ADX_MFE_KERNEL");
+    return e && std::strcmp(e, "rows") == 0;
 }
 
 hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
@@ -1933,9 +1892,8 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         KArgs k16 = ka;
         k16.T = ka.T16;
         k16.X = ka.X16;
-        const int kc = mfe_kernel_choice();
-        hipError_t e = (kc == 2 && mfe_quad_lds(k16) > 0)    ? launch_mfe_quad(k16, seqs, W, scores, terms, dG, mask, stream)
-                       : (kc >= 1 && mfe_cells_lds(k16) > 0) ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
+        hipError_t e = (!mfe_rows_forced() && mfe_cells_lds(k16) > 0)
+                           ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
                            : launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         if (e != hipSuccess) return e;
         KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state

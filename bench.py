@@ -148,8 +148,7 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
 def mfe_kernel_label():
     """The MFE fold kernel the engine launches (kernels.hip mfe_kernel_choice)."""
     k = os.environ.get("ADX_MFE_KERNEL", "cells")
-    return {"rows": "score_kernel<MinPlus16> (lanes = terms)",
-            "quad": "mfe_quad_kernel (lanes = cells, 4 folds per cell)"}.get(
+    return {"rows": "score_kernel<MinPlus16> (lanes = terms)"}.get(
         k, "mfe_cells_kernel (lanes = cells, 2 folds per cell)") + " + FP32 MinPlus fallback launch"
 
 

@@ -14,8 +14,11 @@
  *      (scoring.hh:42-55, ViennaRnaFold scoring.cc:17-103);
  *
  *  (2) the batched Monte Carlo layer adx_ctx_* / adx_walkers_* / adx_run_steps
- *      / adx_score_batch -- thousands of independent walkers, each step of
- *      MonteCarlo::apply (sampling.cc:55-99) fused into one HIP kernel.
+ *      / adx_score_batch -- thousands of independent walkers in lockstep;
+ *      each step of MonteCarlo::apply (sampling.cc:55-99) is three launches
+ *      on one stream, no host round trip: propose (move + thermostat + RNG),
+ *      fold + score of the changed walkers, Metropolis accept (plus the
+ *      outside pass when base-pair terms are scored).
  */
 #ifndef ADDAPT_GPU_H
 #define ADDAPT_GPU_H

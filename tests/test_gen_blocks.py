@@ -1,7 +1,7 @@
 """Host checks of the interior-loop shape generator (tools/gen_mfe_blocks.py)
-behind mfe_cells.hip / mfe_quad.hip: every loop size in exactly one block,
+behind mfe_cells.hip: every loop size in exactly one block,
 the sliced blocks' lane slices cover every generic shape exactly once with the
-right Ninio index, and the committed .inc files are the generator's output."""
+right Ninio index, and the committed .inc file is the generator's output."""
 import filecmp
 import importlib.util
 import os
@@ -19,8 +19,6 @@ def test_partitions_cover_each_loop_size_once():
     sizes = sorted(u for b in blocks for u in b)
     assert sizes == list(range(G.MAXLOOP + 1))
     assert len(blocks) == G.NBLK and max(load) - min(load) <= 10
-    pairs, _ = G.partition_pairs()
-    assert sorted(u for b in pairs for u in b) == list(range(G.MAXLOOP + 1))
 
 
 def test_shape_kinds():
@@ -54,5 +52,5 @@ def test_committed_blocks_match_generator(tmp_path):
     env = dict(os.environ, ADX_GEN_OUT=str(tmp_path))
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_mfe_blocks.py")], env=env,
                           stderr=subprocess.DEVNULL)
-    for name in ("mfe_blocks.inc", "mfe_quad_blocks.inc"):
-        assert filecmp.cmp(str(tmp_path / name), os.path.join(ROOT, "addapt_amd", "csrc", name), shallow=False), name
+    name = "mfe_blocks.inc"
+    assert filecmp.cmp(str(tmp_path / name), os.path.join(ROOT, "addapt_amd", "csrc", name), shallow=False), name

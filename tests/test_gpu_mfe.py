@@ -307,3 +307,38 @@ def test_fold_mfe_nonzero_mlbase(native, oracle, tmp_path):
     # and the default (MLbase = 0) parameters give a different answer somewhere
     s = rand_seq(rng, 100)
     assert oracle.mfe_energy(s, params=OP) >= oracle.mfe_energy(s)
+
+
+@pytest.mark.parametrize("kernel", ["rows", "cells"])
+def test_mfe_kernels_score_and_trajectory(native, oracle, monkeypatch, kernel):
+    """The general MFE kernel (score_kernel<MinPlus16>, lanes = terms: energy
+    models or lengths the cells kernel does not cover) and the default cells
+    kernel, selected per launch by ADX_MFE_KERNEL: scored folds bit-exact and an
+    incremental trajectory identical to the oracle's."""
+    monkeypatch.setenv("ADX_MFE_KERNEL", kernel)
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    eng = _engine(native, tmpl, [active], terms,
+                  thermostat=native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30))
+    seqs = workloads.walker_sequences(tmpl, [active], 16)
+    _, _, dg = eng.score_batch(seqs)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(16):
+            ref = oracle.mfe_energy(seqs[w], active if mac >= 0 else None, motif if cond == 1 else None)
+            assert _same(dg[w, v], ref), (kernel, v, w, dg[w, v], ref)
+    seeds = [11, 12, 13, 14]
+    eng.walkers_init(seeds, seqs[:4])
+    steps = 25
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=1e-12)
+        assert list(tr["position"][:, w]) == ref["pos"], (kernel, w)
+        assert list(tr["outcome"][:, w]) == ref["outcome"], (kernel, w)
+        assert final[w].upper() == ref["seq"].upper(), (kernel, w)
+        assert list(counters[w]) == ref["counters"], (kernel, w)

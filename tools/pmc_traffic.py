@@ -15,8 +15,8 @@ import csv
 import json
 import sys
 
-# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip, mfe_quad.hip)
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "mfe_quad_kernel")
+# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip)
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel")
 
 
 def per_kernel(path, counter):

@@ -14,8 +14,8 @@ import csv
 import json
 import sys
 
-# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip, mfe_quad.hip)
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "mfe_quad_kernel")
+# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip)
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel")
 
 path = sys.argv[1]
 last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 10
