@@ -431,6 +431,7 @@ struct Problem {
     bool mfe_cells_ok = false;   // Ninio saturated from |n1-n2| = 5 on, MLbase >= 0 (mfe_cells.hip)
     // incremental-fold state of the MC walkers (kernels.hip Inc)
     DevBuf<float> dTab;
+    DevBuf<float> dGstep;        // [W][n_variants] (pair terms: score before the outside pass)
     DevBuf<uint8_t> dCur, dValid;
     DevBuf<int> dChg;
     size_t tab_slot = 0;
@@ -493,6 +494,7 @@ struct Problem {
         ka.cur_slot = st ? dCur.p : nullptr;
         ka.tab_valid = st ? dValid.p : nullptr;
         ka.chg = st ? dChg.p : nullptr;
+        ka.gstep = st && !pairs.empty() ? dGstep.p : nullptr;
         return ka;
     }
 
@@ -558,6 +560,7 @@ struct Problem {
         HIP_TRY(dCur.alloc(W));
         HIP_TRY(dValid.alloc(W));
         HIP_TRY(dChg.alloc(size_t(W) * 2));
+        if (!pairs.empty()) HIP_TRY(dGstep.alloc(size_t(W) * variants.size()));
         HIP_TRY(hipMemsetAsync(dCur.p, 1, W, stream));     // the initial fold writes slot 0
         HIP_TRY(hipMemsetAsync(dValid.p, 0, W, stream));
         HIP_TRY(hipMemsetAsync(dChg.p, 0xff, sizeof(int) * 2 * W, stream));

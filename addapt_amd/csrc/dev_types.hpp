@@ -171,6 +171,10 @@ struct KArgs {
     uint8_t *cur_slot;
     uint8_t *tab_valid;
     const int *chg;
+    // [W][n_variants] per-variant energies of the step's proposals when the score
+    // waits for the outside pass (pair terms): score_kernel -> bppm_kernel
+    // (re-using the inside tables just written) -> combine_kernel
+    float *gstep;
 };
 
 // Monte Carlo state (device, read/write).

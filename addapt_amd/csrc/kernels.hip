@@ -1161,7 +1161,9 @@ __device__ double combine_score(const KArgs &ka, const Lds<P> &L, const double *
             const DevTermMap m = ka.tmap[c * ka.n_terms + t];
             double p;
             if (m.kind == 1) {
-                p = pp[m.pidx];   // RnaFold::base_pair_prob (scoring.cc:37-51), bppm_kernel
+                // RnaFold::base_pair_prob (scoring.cc:37-51), bppm_kernel; null: the
+                // score waits for the outside pass (combine_kernel recomputes it)
+                p = pp ? pp[m.pidx] : 0.5;
             } else {
                 // vrna_pf returns float (scoring.cc:58,65)
                 const double gt = static_cast<double>(static_cast<float>(L.G[m.vfree]));
@@ -1558,10 +1560,13 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
 // One workgroup per (walker, outside variant): inside (pf_group, P = 1) then
 // outside.  full: [W][n_bvars][ld*ld] or null; pair_p: [W][n_pairs] or null;
 // GOUT: gscratch holds gridDim.x slices of outs_global_bytes.
+// reuse: the proposal's inside tables were just written by score_kernel to the
+// walker's next slot (KArgs::tab, score P = sp): pf_group restores every cell
+// from there (an incremental fold with nothing changed) instead of refolding.
 template <int NT, bool GOUT>
 __global__ void __launch_bounds__(NT, 1)
 bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
-            double *full, int ld, double *pair_p, char *gscratch) {
+            double *full, int ld, double *pair_p, char *gscratch, int sp, int reuse) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<1> L;
     const size_t o = lds_layout<false, 1>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, 0, false);
@@ -1578,7 +1583,22 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
     const int vs[1] = {v};
     float z[1];
     bool bad = false;
-    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z, bad, Inc{nullptr, nullptr, 0, 0});
+    Inc inc{nullptr, nullptr, 0, 0};
+    if (reuse && ka.tab) {
+        const size_t B = 3 * size_t(ka.cells) + size_t(ka.Nmax) + 2;   // one variant's tables
+        size_t o = size_t(v) * B;                                      // score P = 1: group = variant
+        if (sp == 2) {
+            for (int g = 0; g < ka.n_groups2; g++) {
+                if (ka.groups2[2 * g] == v) { o = size_t(g) * 2 * B; break; }
+                if (ka.groups2[2 * g + 1] == v) { o = size_t(g) * 2 * B + B; break; }
+            }
+        }
+        const int cur = ka.cur_slot[w];
+        inc.src = ka.tab + size_t(w) * 2 * ka.tab_slot + size_t(1 - cur) * ka.tab_slot + o;
+        inc.m_lo = 4 * ka.Nmax + 8;   // no changed cell: every cell and q5 from src
+        inc.m_hi = -8;
+    }
+    pf_group<NT, 1, SumProd>(ka, vs, L.raw, L, XS, z, bad, inc);
     __syncthreads();
     outside<NT>(ka, v, bv, L, O, XS, z[0],
                 full ? full + (size_t(w) * ka.n_bvars + bv) * size_t(ld) * ld : nullptr, ld,
@@ -1937,7 +1957,8 @@ size_t bppm_scratch_bytes(const KArgs &ka, int W) {
 
 template <bool GOUT>
 static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs, int W, const int *mask,
-                                double *full, int ld, double *pair_p, char *scratch, hipStream_t stream) {
+                                double *full, int ld, double *pair_p, char *scratch, hipStream_t stream,
+                                bool reuse) {
     auto k = bppm_kernel<512, GOUT>;
     static size_t configured = 0;
     if (lds > configured) {
@@ -1947,18 +1968,49 @@ static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs
         configured = lds;
     }
     hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p,
-                       scratch);
+                       scratch, choose_p(ka), reuse ? 1 : 0);
     return hipGetLastError();
+}
+
+static hipError_t launch_bppm_r(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
+                                double *pair_p, char *scratch, hipStream_t stream, bool reuse) {
+    bool gout = false;
+    const size_t lds = bppm_lds_bytes(ka, &gout);
+    if (lds == 0 || ka.n_bvars <= 0 || (gout && !scratch)) return hipErrorInvalidValue;
+    if (gout) return launch_bppm_t<true>(ka, lds, seqs, W, mask, full, ld, pair_p, scratch, stream, reuse);
+    return launch_bppm_t<false>(ka, lds, seqs, W, mask, full, ld, pair_p, nullptr, stream, reuse);
 }
 
 // scratch: bppm_scratch_bytes(ka, W) bytes of device memory (null when 0)
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
                        double *pair_p, char *scratch, hipStream_t stream) {
-    bool gout = false;
-    const size_t lds = bppm_lds_bytes(ka, &gout);
-    if (lds == 0 || ka.n_bvars <= 0 || (gout && !scratch)) return hipErrorInvalidValue;
-    if (gout) return launch_bppm_t<true>(ka, lds, seqs, W, mask, full, ld, pair_p, scratch, stream);
-    return launch_bppm_t<false>(ka, lds, seqs, W, mask, full, ld, pair_p, nullptr, stream);
+    return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
+}
+
+// Scores of the step's proposals once the outside pass has written the pair
+// probabilities: combine_score over the per-variant energies score_kernel left
+// in KArgs::gstep (one thread per walker).
+__global__ void combine_kernel(KArgs ka, int W, const int *mask, double *scores, double *terms) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W || (mask && mask[w] != 1)) return;
+    const float *g = ka.gstep + size_t(w) * ka.n_variants;
+    const double *pp = ka.pair_p + size_t(w) * ka.n_pairs;
+    const int nt = ka.n_terms * ka.n_ctx_eff;
+    double *tv = terms ? terms + size_t(w) * nt : nullptr;
+    const DevScaled &X = *ka.X;
+    double score = 0.0;
+    for (int c = 0; c < ka.n_ctx_eff; c++) {
+        for (int t = 0; t < ka.n_terms; t++) {
+            const DevTermMap m = ka.tmap[c * ka.n_terms + t];
+            double p = (m.kind == 1) ? pp[m.pidx]
+                                     : exp((static_cast<double>(g[m.vfree]) - static_cast<double>(g[m.vcons])) / X.kT);
+            if (!m.favorable) p = 1.0 - p;
+            const double val = log(p);
+            if (tv) tv[c * ka.n_terms + t] = val;
+            score += m.weight * val;
+        }
+    }
+    scores[w] = score;
 }
 
 // evs (optional): 2 * nsteps events recorded around each step's score launch
@@ -1970,12 +2022,28 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         // the event window covers the outside pass too when the terms read base-pair
         // probabilities (bench.py divides bppm + score work by it)
         if (evs) (void)hipEventRecord(evs[2 * s], stream);
-        if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
-            hipError_t e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0,
-                                       const_cast<double *>(ka.pair_p), ka.bppm_scratch, stream);
+        hipError_t e;
+        if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
+            // inside folds first (they write the proposal's tables), then the outside
+            // pass on those tables, then the scores with the pair probabilities
+            KArgs ki = ka;
+            ki.pair_p = nullptr;
+            e = launch_score_m(ki, st.prop_seq, st.W, st.prop_score, nullptr, ka.gstep, st.changed, stream);
             if (e != hipSuccess) return e;
+            e = launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
+                              ka.bppm_scratch, stream, true);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, st.changed,
+                               st.prop_score, tv);
+            e = hipGetLastError();
+        } else {
+            if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
+                e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
+                                ka.bppm_scratch, stream);
+                if (e != hipSuccess) return e;
+            }
+            e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         }
-        hipError_t e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
         if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,

@@ -142,3 +142,33 @@ def test_mc_trajectory_with_pair_terms(native, oracle):
         assert list(tr["outcome"][:, w]) == ref["outcome"], w
         assert final[w].upper() == ref["seq"].upper(), w
         assert list(counters[w]) == ref["counters"]
+
+
+@pytest.mark.parametrize("N", [100, 150])
+def test_mc_pair_terms_proposed_scores(native, oracle, N):
+    """Configs 3 / 4 shape (N = 100: outside tables in LDS; N = 150: global
+    scratch): inside folds first, the outside pass on the proposal's stored
+    inside tables, then the scores.  Every scored proposal's score matches the
+    oracle's from-scratch score of that proposal (ln p terms within 2e-3)."""
+    tmpl, active = workloads.synthetic(N)
+    terms = _objective(N)
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [21, 22, 23]
+    seqs = workloads.walker_sequences(tmpl, [active], 64)
+    eng.walkers_init(seeds + list(range(100, 161)), seqs)
+    steps = 10
+    tr = eng.run_steps(steps, trace=True)
+    _, _, counters = eng.download()
+    assert (counters.sum(axis=1) == steps).all()
+    sf = _oracle_sf(oracle, terms)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=2e-3)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                a, b = tr["proposed_score"][s, w], ref["proposed_score"][s]
+                assert a == b or abs(a - b) <= 2e-3 * max(1.0, abs(b)), (N, w, s, a, b)
