@@ -1981,6 +1981,10 @@ static hipError_t launch_bppm_r(const KArgs &ka, const uint8_t *seqs, int W, con
     return launch_bppm_t<false>(ka, lds, seqs, W, mask, full, ld, pair_p, nullptr, stream, reuse);
 }
 
+size_t outside_cells_lds(const KArgs &ka);
+hipError_t launch_outside_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *pair_p,
+                                int sp_score, hipStream_t stream);
+
 // scratch: bppm_scratch_bytes(ka, W) bytes of device memory (null when 0)
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
                        double *pair_p, char *scratch, hipStream_t stream) {
@@ -2030,8 +2034,15 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
             ki.pair_p = nullptr;
             e = launch_score_m(ki, st.prop_seq, st.W, st.prop_score, nullptr, ka.gstep, st.changed, stream);
             if (e != hipSuccess) return e;
-            e = launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
-                              ka.bppm_scratch, stream, true);
+            // lanes = cells outside kernel (outside_cells.hip) where it covers the
+            // length, else bppm_kernel on the same stored tables
+            const char *ok = std::getenv("ADX_OUTSIDE_KERNEL");
+            const bool old = ok && std::strcmp(ok, "bppm") == 0;
+            e = (!old && outside_cells_lds(ka) > 0)
+                    ? launch_outside_cells(ka, st.prop_seq, st.W, st.changed, const_cast<double *>(ka.pair_p),
+                                           choose_p(ka), stream)
+                    : launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
+                                    ka.bppm_scratch, stream, true);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, st.changed,
                                st.prop_score, tv);

@@ -144,14 +144,21 @@ def test_mc_trajectory_with_pair_terms(native, oracle):
         assert list(counters[w]) == ref["counters"]
 
 
-@pytest.mark.parametrize("N", [100, 150])
-def test_mc_pair_terms_proposed_scores(native, oracle, N):
-    """Configs 3 / 4 shape (N = 100: outside tables in LDS; N = 150: global
-    scratch): inside folds first, the outside pass on the proposal's stored
-    inside tables, then the scores.  Every scored proposal's score matches the
-    oracle's from-scratch score of that proposal (ln p terms within 2e-3)."""
+@pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (150, False)])
+def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
+    """Configs 3 / 4 shape: inside folds first, the outside pass on the
+    proposal's stored inside tables (N <= 128: outside_cells_kernel, lanes =
+    cells; N = 150: bppm_kernel with global scratch), then the scores.  Every
+    scored proposal's score matches the oracle's from-scratch score of that
+    proposal (ln p terms within 2e-3).  motif_pairs: pair terms inside the
+    ligand motif (credited from the motif's closing cell in the holo fold)."""
     tmpl, active = workloads.synthetic(N)
     terms = _objective(N)
+    if motif_pairs:
+        o = (N - 27) // 2   # the aptamer's site in the synthetic template
+        terms = workloads.default_objective() + [("holo", ("pair", o + 4, o + 22), True, 1.0),
+                                                ("apo", ("pair", o, o + 26), False, 0.5),
+                                                ("holo", ("pair", o + 7, o + 16), True, 0.25)]
     th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
     eng = _engine(native, tmpl, [active], terms, thermostat=th)
     seeds = [21, 22, 23]
