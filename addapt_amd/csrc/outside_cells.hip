@@ -12,8 +12,11 @@
 //     (i, i+d), so every interior-loop shape (n1, n2) is one LDS read per lane of
 //     the outer cell (i-1-n1, j+1+n2) at a per-lane base plus an immediate
 //     offset, no cross-lane reduction.  The 496 shapes are split by loop size
-//     over 12 waves (B); waves 12-15 sum the multiloop adjoints (M); the next
-//     step finalizes the cell (F).
+//     over 10 waves (B); waves 10-15 sum the multiloop adjoints (M) over row- /
+//     column-major copies of Y, qm1 and qm (consecutive rows / columns of a
+//     triangular table start in distinct banks, so a split point is one
+//     conflict-free read per lane at an immediate offset); the next step
+//     finalizes the cell (F).
 //
 //   q5b[m]    = sigma q5b[m+1] + sum_j q5b[j] qb(m+1,j) ext(m+1,j)   (before the sweep)
 //   qmb(i,j)  = sum_{l >= j+5} Y(i,l) qm1(j+1,l)                      (M)
@@ -25,43 +28,63 @@
 //   P(i,j)    = qb(i,j) qbb(i,j) / Z
 //
 // Covered: unconstrained folds (the pair terms' folds are the conditions'
-// unconstrained folds, adx_api.cpp), N <= 128 (LDS); everything else takes
+// unconstrained folds, adx_api.cpp), N <= 112 (LDS); everything else takes
 // kernels.hip bppm_kernel.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 
 #include "dev_types.hpp"
 #include "fold_common.hpp"
 
 namespace adx {
+
+#ifdef ADX_STAMP
+// Diagnostic build only: per-wave cycle sums of the phases (s_memtime), read
+// back through adx_debug_stamps_outside().  Never in the product.
+__device__ unsigned long long g_stamps_o[16][8];
+#define OSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define OSTAMP(k) do { } while (0)
+#endif
+
 namespace {
 
 constexpr int OX_NW = 16;             // waves per workgroup
 constexpr int OX_NT = OX_NW * WAVE;
-constexpr int OX_NB = 12;             // interior-loop blocks (waves 0..11)
+constexpr int OX_NB = 10;             // interior-loop blocks (waves 0..9)
+constexpr int OX_NM = OX_NW - OX_NB;  // multiloop-sum waves (10..15)
 constexpr int OX_WIN = 32;            // qbb window: spans d+2 .. d+32 are read at step d
 constexpr int OX_PAD = 32;            // zero cells in front of each window row (outer a >= i-31)
 constexpr int OX_MAXP = 64;           // requested pairs of one fold kept in LDS
-constexpr int OX_NMAX = 128;
+constexpr int OX_NMAX = 112;
+constexpr int OX_SLACK = 64;          // zeroed floats after each cell table (reads past a row end)
+constexpr int OX_FF = 5;              // finalize record fields (see frec_write)
+constexpr int OX_RF = 9;              // cell setup record fields (see rec_write)
 
 // LDS carve for folded length N (runtime; the host sizes the launch with it)
 struct OxLay {
     int C, NP, RL;
-    size_t Y, QM, QM1, QW, OW, PART, MLP, RQ, RR, R1, Q5, Q5B, PM, CT, DT, PD, S, MT, BYTES;
+    size_t YR, YC, Q1R, QMC, QW, OW, PART, MLP, REC, FR, SF, RQ, RR, R1, Q5, Q5B, PM, CT, DT, PD, PL, S, MT, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit OxLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
         NP = N + 2;
         RL = N + 2 * OX_PAD;
         size_t o = 0;
-        Y = o;    o += a16(size_t(C) * 4);                       // Y (qbm_in before the sweep)
-        QM = o;   o += a16(size_t(C) * 4);                       // inside qm, diagonal-major
-        QM1 = o;  o += a16(size_t(C) * 4);                       // inside qm1, diagonal-major
+        const size_t T = a16((size_t(C) + OX_SLACK) * 4);
+        YR = o;   o += T;                                        // Y row-major (qmb sums)
+        YC = o;   o += T;                                        // Y column-major (r2 sums; G before the sweep)
+        Q1R = o;  o += T;                                        // inside qm1, row-major
+        QMC = o;  o += T;                                        // inside qm, column-major
         QW = o;   o += a16(size_t(OX_WIN) * RL * 4);             // qbb * mismatchI(outer) window
         OW = o;   o += a16(size_t(OX_WIN) * RL);                 // outer codes window
         PART = o; o += a16(size_t(2) * 2 * OX_NB * WAVE * 4);   // [parity][lane-set][block][lane]
-        MLP = o;  o += a16(size_t(2) * 4 * WAVE * 4);           // [parity][M wave][lane]
+        MLP = o;  o += a16(size_t(2) * OX_NM * WAVE * 4);       // [parity][M wave][lane]
+        REC = o;  o += a16(size_t(2) * 2 * OX_RF * WAVE * 4);   // cell setup records [parity][lane-set][field][lane]
+        FR = o;   o += a16(size_t(2) * 2 * OX_FF * WAVE * 4);   // finalize records [parity][lane-set][field][lane]
+        SF = o;   o += a16(size_t(31) * 32 * 4);                 // constant factor of shape (u, n1): [u][n1]
         RQ = o;   o += a16(size_t(2) * NP * 4);                  // qmb ring [parity][i]
         RR = o;   o += a16(size_t(2) * NP * 4);                  // R ring
         R1 = o;   o += a16(size_t(2) * NP * 4);                  // qm1b ring
@@ -71,6 +94,7 @@ struct OxLay {
         CT = o;   o += a16(size_t(CT_SIZE) * 4);
         DT = o;   o += a16(size_t(DT_EXT + 288) * 4);            // MMI, MLS, EXT
         PD = o;   o += a16(size_t(OX_MAXP) * 8);                 // requested pairs: qb qbb / Z
+        PL = o;   o += a16(size_t(OX_MAXP) * 4 + 4);             // this fold's pairs: t | i << 8 | j << 16; count
         S = o;    o += a16(size_t(NP) + 8);
         MT = o;   o += a16(size_t(NP));                          // motif site flags
         BYTES = o;
@@ -78,13 +102,31 @@ struct OxLay {
 };
 
 struct OxL {
-    float *Y, *qm, *qm1, *qw, *part, *mlp, *rq, *rr, *r1, *q5, *q5b, *pm, *ct, *dt;
+    float *yr, *yc, *q1r, *qmc, *qw, *part, *mlp, *rec, *fr, *sf, *rq, *rr, *r1, *q5, *q5b, *pm, *ct, *dt;
+    int *pl;
     uint8_t *ow, *S, *mat;
     double *pd;
     int RL, NP;
 };
 
 __device__ __forceinline__ int wslot(int D) { return D & (OX_WIN - 1); }
+
+// diagonal D of the diagonal-major cell index k: off(D) <= k < off(D + 1)
+__device__ __forceinline__ int inv_off(int k, int N) {
+    const float b = float(2 * N - 7);
+    int D = 4 + int((b - sqrtf(fmaxf(b * b - 8.f * float(k), 0.f))) * 0.5f);
+    D = D < 4 ? 4 : D;
+    while (D < N - 1 && off(D + 1, N) <= k) D++;
+    while (D > 4 && off(D, N) > k) D--;
+    return D;
+}
+// column j of the column-major cell index k: colb(j) <= k < colb(j + 1)
+__device__ __forceinline__ int inv_colb(int k) {
+    int j = 5 + int((sqrtf(8.f * float(k) + 1.f) - 1.f) * 0.5f);
+    while (colb(j + 1) <= k) j++;
+    while (colb(j) > k) j--;
+    return j;
+}
 
 // interior-loop shape kinds (dev_types.hpp TermKind; -1 = generic)
 __host__ __device__ constexpr int okind(int n1, int n2) {
@@ -106,69 +148,127 @@ struct OxCell {                 // per lane: the inner pair (i, j) of every shap
     float t11, t12, t21, t22;   // 1x1 / 1x2 / 2x1 / 2x2 table factors (HBM, issued at the block start)
 };
 
-// Shapes of loop size U for the lane's cell; qw / ow: this lane's window row of
-// the outer span d + 2 + U at outer a = i - 1 - U (n1 = U), so shape n1 reads
-// offset U - n1.
-template <int U>
-__device__ __forceinline__ void oshape(const OxL &L, const DevScaled *__restrict__ XS, const OxCell &c,
-                                       const float *qw, const uint8_t *ow, int ty2, float &g, float &sp) {
-    const float *ct = L.ct;
-#pragma unroll
-    for (int n1 = 0; n1 <= U; n1++) {
-        const int n2 = U - n1;
-        const float v = qw[U - n1];
-        const int k = okind(n1, n2);
-        if (k < 0) {
-            g = fmaf(v, XS->fgen[(U - 6) * FG_ROW + n1 - 2], g);
+// One shape (N1, U - N1) of the lane's cell; qw / ow: this lane's window row of
+// the outer span d + 2 + U at outer a = i - 1 - U (n1 = U), so shape N1 reads
+// offset U - N1; fv: the shapes' constant factors (OxL::sf row U, in registers).
+// Compile-time shape: the kind and every table offset fold.
+template <int U, int N1>
+__device__ __forceinline__ void oshape1(const OxL &L, const OxCell &c, const float *fv, const float *qw,
+                                        const uint8_t *ow, int ty2, float &g, float &sp) {
+    constexpr int k = okind(N1, U - N1);
+    const float v = qw[U - N1];
+    if constexpr (k < 0) {
+        g = fmaf(v, fv[N1], g);
+    } else {
+        const float *ct = L.ct;
+        const int oc = ow[U - N1];
+        float f;
+        if constexpr (k == TK_STK || k == TK_B1) {
+            f = ct[CT_INVMM + oc] * ct[CT_STK + ((oc * 41) >> 10) * 8 + ty2] * fv[N1];
+        } else if constexpr (k == TK_BUL) {
+            f = ct[CT_BUL + oc] * (c.tau_in * fv[N1]);
+        } else if constexpr (k == TK_1N) {
+            f = ct[CT_ONEN + oc] * (c.mo_in * fv[N1]);
+        } else if constexpr (k == TK_M23) {
+            f = ct[CT_INVMM + oc] * ct[CT_M23O + oc] * (c.m23_in * fv[N1]);
         } else {
-            const int oc = ow[U - n1];
-            float f;
-            if (k == TK_STK || k == TK_B1) {
-                f = ct[CT_INVMM + oc] * ct[CT_STK + ((oc * 41) >> 10) * 8 + ty2] * XS->ctab[CT_FSM + (k == TK_B1 ? 1 : 0)];
-            } else if (k == TK_BUL) {
-                f = ct[CT_BUL + oc] * (c.tau_in * XS->ctab[CT_FB + U]);
-            } else if (k == TK_1N) {
-                f = ct[CT_ONEN + oc] * (c.mo_in * XS->ctab[CT_F1N + U - 1]);
-            } else if (k == TK_M23) {
-                f = ct[CT_INVMM + oc] * ct[CT_M23O + oc] * (c.m23_in * XS->ctab[CT_FSM + 5]);
-            } else {
-                const float tv = k == TK_I11 ? c.t11 : k == TK_I12 ? c.t12 : k == TK_I21 ? c.t21 : c.t22;
-                const int fs = k == TK_I11 ? 2 : k == TK_I22 ? 4 : 3;
-                f = ct[CT_INVMM + oc] * (tv * XS->ctab[CT_FSM + fs]);
+            const float tv = k == TK_I11 ? c.t11 : k == TK_I12 ? c.t12 : k == TK_I21 ? c.t21 : c.t22;
+            f = ct[CT_INVMM + oc] * (tv * fv[N1]);
+        }
+        sp = fmaf(v, f, sp);
+    }
+}
+template <int U, int... N1s>
+__device__ __forceinline__ void oshape_seq(std::integer_sequence<int, N1s...>, const OxL &L, const OxCell &c,
+                                           const float *fv, const float *qw, const uint8_t *ow, int ty2, float &g,
+                                           float &sp) {
+    (oshape1<U, N1s>(L, c, fv, qw, ow, ty2, g, sp), ...);
+}
+// the shapes of loop size U (skipped past the step's umax: uniform)
+template <int U>
+struct OxSize {
+    float fv[U < 0 ? 1 : U + 1];
+    __device__ __forceinline__ void load(const OxL &L) {
+        if constexpr (U >= 0)
+#pragma unroll
+            for (int n1 = 0; n1 <= U; n1++) fv[n1] = L.sf[U * 32 + n1];
+    }
+    __device__ __forceinline__ void run(const OxL &L, const OxCell &c, int d, int umax, int ty2, float &g,
+                                        float &sp) const {
+        if constexpr (U >= 0) {
+            if (U <= umax) {
+                const int o = wslot(d + 2 + U) * L.RL + OX_PAD + c.i - 2 - U;
+                oshape_seq<U>(std::make_integer_sequence<int, U + 1>{}, L, c, fv, L.qw + o, L.ow + o, ty2, g, sp);
             }
-            sp = fmaf(v, f, sp);
         }
     }
-}
+};
 
-// one loop size of a block: skipped past the step's umax (uniform)
-#define OX_U(U)                                                                                   \
-    if ((U) <= umax) {                                                                            \
-        const int o = wslot(d + 2 + (U)) * L.RL + OX_PAD + c.i - 2 - (U);                         \
-        oshape<(U)>(L, XS, c, L.qw + o, L.ow + o, ty2, g, sp);                                    \
-    }
+#ifdef ADX_STAMP
+#define OX_STP_PARAMS , unsigned long long *st_acc, unsigned long long &st_last
+#define OX_STP_ARGS , st_acc, st_last
+#else
+#define OX_STP_PARAMS
+#define OX_STP_ARGS
+#endif
 
-// blocks of loop sizes of about equal cost (generic shape ~2 instructions, a
-// special ~9); the 1x1..2x2 table shapes (u = 2, 3, 4) share blocks with large
-// loops so the table loads issued at the block start land meanwhile
-__device__ __forceinline__ void oblock(int b, const OxL &L, const DevScaled *__restrict__ XS, const OxCell &c,
-                                       int d, int umax, int ty2, float &g, float &sp) {
-    switch (b) {
-        case 0: OX_U(8) OX_U(30) break;
-        case 1: OX_U(9) OX_U(29) break;
-        case 2: OX_U(10) OX_U(28) break;
-        case 3: OX_U(11) OX_U(27) break;
-        case 4: OX_U(12) OX_U(26) break;
-        case 5: OX_U(25) OX_U(5) OX_U(4) break;
-        case 6: OX_U(7) OX_U(13) OX_U(24) break;
-        case 7: OX_U(6) OX_U(14) OX_U(23) break;
-        case 8: OX_U(22) OX_U(15) OX_U(3) break;
-        case 9: OX_U(21) OX_U(16) OX_U(2) break;
-        case 10: OX_U(1) OX_U(17) OX_U(20) break;
-        default: OX_U(0) OX_U(18) OX_U(19) break;
+// B: the interior-loop gather of every diagonal for one block of loop sizes
+// (U3..U0, -1 = none), the block's shape factors held in registers for the
+// whole sweep; one barrier per diagonal, as the M / F waves.
+template <int U0, int U1, int U2, int U3, class Fin>
+__device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, const Fin &fin OX_STP_PARAMS) {
+    constexpr bool TB = (U0 >= 2 && U0 <= 4) || (U1 >= 2 && U1 <= 4) || (U2 >= 2 && U2 <= 4) || (U3 >= 2 && U3 <= 4);
+    OxSize<U0> s0;
+    OxSize<U1> s1;
+    OxSize<U2> s2;
+    OxSize<U3> s3;
+    s0.load(L);
+    s1.load(L);
+    s2.load(L);
+    s3.load(L);
+    for (int d = N - 1; d >= 3; d--) {
+        const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
+        const int par = d & 1;
+        const int umax = min(30, N - 3 - d);                      // outer spans d+2 .. d+2+umax
+        for (int ls = 0; ls < nls; ls++) {
+            int i = 1 + ls * WAVE + lane;
+            if (i > N - d) i = N - d;
+            const float *r = L.rec + ((par * 2 + ls) * OX_RF) * WAVE + lane;
+            const int tp = __float_as_int(r[8 * WAVE]);
+            float *pout = L.part + ((par * 2 + ls) * OX_NB + wid) * WAVE + lane;
+            if (umax < 0 || __ballot(tp >= 256) == 0) {   // no outer loop fits (or nothing pairs)
+                *pout = 0.f;
+                continue;
+            }
+            OxCell c;
+            c.i = i;
+            const int ty2 = tp & 255;
+            c.mmin = r[0];
+            c.tau_in = r[WAVE];
+            c.mo_in = r[2 * WAVE];
+            c.m23_in = r[3 * WAVE];
+            c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
+            if constexpr (TB) {
+                c.t11 = r[4 * WAVE];
+                c.t12 = r[5 * WAVE];
+                c.t21 = r[6 * WAVE];
+                c.t22 = r[7 * WAVE];
+            }
+            float g = 0.f, sp = 0.f;
+            OSTAMP(2);   // B cell setup
+            s0.run(L, c, d, umax, ty2, g, sp);
+            s1.run(L, c, d, umax, ty2, g, sp);
+            s2.run(L, c, d, umax, ty2, g, sp);
+            s3.run(L, c, d, umax, ty2, g, sp);
+            OSTAMP(3);   // B shapes
+            *pout = fmaf(g, c.mmin, sp);
+        }
+        fin(d);   // F of diagonal d + 1 on waves 0 and 1
+        OSTAMP(5);
+        lds_barrier();
+        OSTAMP(6);   // barrier
     }
 }
-constexpr unsigned OX_TABLE_BLOCKS = (1u << 5) | (1u << 8) | (1u << 9);   // blocks with u = 4 / 3 / 2
 
 __device__ __forceinline__ float wave_sum_f(float v) {
 #pragma unroll
@@ -189,13 +289,18 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     const int N = uni(V.N);
     const OxLay Y(N);
     OxL L;
-    L.Y = reinterpret_cast<float *>(smem + Y.Y);
-    L.qm = reinterpret_cast<float *>(smem + Y.QM);
-    L.qm1 = reinterpret_cast<float *>(smem + Y.QM1);
+    L.yr = reinterpret_cast<float *>(smem + Y.YR);
+    L.yc = reinterpret_cast<float *>(smem + Y.YC);
+    L.q1r = reinterpret_cast<float *>(smem + Y.Q1R);
+    L.qmc = reinterpret_cast<float *>(smem + Y.QMC);
+    L.pl = reinterpret_cast<int *>(smem + Y.PL);
     L.qw = reinterpret_cast<float *>(smem + Y.QW);
     L.ow = reinterpret_cast<uint8_t *>(smem + Y.OW);
     L.part = reinterpret_cast<float *>(smem + Y.PART);
     L.mlp = reinterpret_cast<float *>(smem + Y.MLP);
+    L.rec = reinterpret_cast<float *>(smem + Y.REC);
+    L.sf = reinterpret_cast<float *>(smem + Y.SF);
+    L.fr = reinterpret_cast<float *>(smem + Y.FR);
     L.rq = reinterpret_cast<float *>(smem + Y.RQ);
     L.rr = reinterpret_cast<float *>(smem + Y.RR);
     L.r1 = reinterpret_cast<float *>(smem + Y.R1);
@@ -211,6 +316,10 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     L.NP = Y.NP;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
     const int C = Y.C, NP = Y.NP;
+#ifdef ADX_STAMP
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
     const DevTables &T = *ka.T;
 
     // ---- the proposal's inside tables (score_kernel's P = sp_score layout, kernels.hip Inc)
@@ -253,22 +362,26 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         L.dt[DT_MLS + k] = (&T.mlstem[0][0][0])[k];
     }
     for (int k = tid; k < 288; k += OX_NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
-    // inside tables: qbm (diagonal-major, as stored) into the Y region for the
-    // exterior adjoint, qm (row-major) and qm1 (column-major) transposed
-    for (int D = 4; D <= N - 1; D++) {
-        const int od = off(D, N);
-        for (int r = tid; r < N - D; r += OX_NT) {
-            const int i = r + 1, j = i + D;
-            L.Y[od + r] = src[od + r];
-            L.qm[od + r] = src[Cs + rowb(i, N) + D - 4];
-            L.qm1[od + r] = src[2 * Cs + colb(j) + i - 1];
+    // constant factor of each shape (u, n1): generic fgen, bulge / 1xn length
+    // factors, the sigma powers of the tabulated loops (adx_api.cpp addS)
+    for (int k = tid; k < 31 * 32; k += OX_NT) {
+        const int u = k >> 5, n1 = k & 31, n2 = u - n1;
+        float f = 0.f;
+        if (n1 <= u) {
+            const int kd = okind(n1, n2);
+            f = kd < 0 ? XS->fgen[(u - 6) * FG_ROW + n1 - 2]
+              : kd == TK_STK ? XS->ctab[CT_FSM + 0]
+              : kd == TK_B1 ? XS->ctab[CT_FSM + 1]
+              : kd == TK_BUL ? XS->ctab[CT_FB + u]
+              : kd == TK_1N ? XS->ctab[CT_F1N + u - 1]
+              : kd == TK_I11 ? XS->ctab[CT_FSM + 2]
+              : kd == TK_I22 ? XS->ctab[CT_FSM + 4]
+              : kd == TK_M23 ? XS->ctab[CT_FSM + 5]
+              : XS->ctab[CT_FSM + 3];   // 1x2 / 2x1
         }
+        L.sf[k] = f;
     }
     for (int k = tid; k <= N; k += OX_NT) L.q5[k] = src[3 * Cs + k];
-    for (int k = tid; k < OX_WIN * L.RL; k += OX_NT) {
-        L.qw[k] = 0.f;
-        L.ow[k] = 0;
-    }
     for (int k = tid; k < 2 * NP; k += OX_NT) L.rq[k] = L.rr[k] = L.r1[k] = 0.f;
     for (int k = tid; k < NP; k += OX_NT) { L.q5b[k] = 0.f; L.pm[k] = 0.f; L.mat[k] = 0; }
     for (int k = tid; k < OX_MAXP; k += OX_NT) L.pd[k] = 0.0;
@@ -284,26 +397,80 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     const bool motif = V.motif != 0 && XS->motif_len > 0;
     const int mL = XS->motif_len;
 
-    // ---- exterior adjoint q5b (one wave, sequential in m; kernels.hip outside())
+    // this fold's requested pairs (score terms), kept in LDS for the finalize
+    if (tid == 0) {
+        int n = 0;
+        for (int t = 0; t < ka.n_pairs && t < OX_MAXP; t++)
+            if (ka.pairs[3 * t] == bv) L.pl[n++] = t | (ka.pairs[3 * t + 1] << 8) | (ka.pairs[3 * t + 2] << 16);
+        L.pl[OX_MAXP] = n;
+    }
+    // inside tables, one flat pass over the cells: qm1 row-major and qm
+    // column-major (transposed from the slot's column- / row-major), Y row-major
+    // zeroed; the exterior factors G(i, j) = qb(i,j) ext(i,j) column-major in the
+    // YC region (zeroed after the exterior adjoint)
+    float *G = L.yc;
+#pragma unroll 2
+    for (int k = tid; k < C + OX_SLACK; k += OX_NT) {
+        if (k >= C) {   // slack after each table: finite zeros for reads past a row end
+            L.yr[k] = L.q1r[k] = L.qmc[k] = G[k] = 0.f;
+            continue;
+        }
+        const int i = inv_off(k, N) - 3, l = i + 4 + (k - rowb(i, N));   // row-major cell (i, l): rowb == off(i + 3)
+        L.q1r[k] = src[2 * Cs + colb(l) + i - 1];
+        L.yr[k] = 0.f;
+        const int jc = inv_colb(k), ic = k - colb(jc) + 1;                 // column-major cell (ic, jc)
+        L.qmc[k] = src[Cs + rowb(ic, N) + jc - ic - 4];
+        const int ty = ptype(S[ic], S[jc]);
+        const int cc = rtype(ty) * 25 + S[jc + 1] * 5 + S[ic - 1];
+        const float e = L.dt[DT_EXT + ty * 36 + ((ic > 1) ? S[ic - 1] : 5) * 6 + ((jc < N) ? S[jc + 1] : 5)];
+        G[k] = src[off(jc - ic, N) + ic - 1] * (ct[CT_INVMM + cc] * e);   // non-pairable: -0 * x = 0
+    }
+    __syncthreads();
+
+    OSTAMP(0);   // loads + table pass
+    // ---- exterior adjoint (kernels.hip outside(), push form, one wave, lanes = m):
+    // once q5b[j] is known every m <= j-5 takes q5b[j] G(m+1, j).  acc[j-5] is
+    // final after the push of j, and q5b[j-5] needs it four steps later, so the
+    // loop-carried chain is one FMA: q5b[j-1] = sigma q5b[j] + acc[j-1], acc[j-1]
+    // read (readlane) four iterations ahead; the next column of G is loaded
+    // during the current push.
     if (wid == 0) {
         const float sig1 = XS->sig[1];
+        float acc0 = 0.f, acc1 = 0.f;   // m = lane, m = 64 + lane
+        float val = 1.f;                // q5b[N]
+        float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;   // acc[j-1], acc[j-2], acc[j-3], acc[j-4]
         if (lane == 0) L.q5b[N] = 1.f;
-        float nxt = 1.f;
-        for (int m = N - 1; m >= 0; m--) {
-            const int k = m + 1;
-            float acc = 0.f;
-            for (int j = k + 4 + lane; j <= N; j += WAVE) {
-                const int ty = ptype(S[k], S[j]);
-                const int cc = rtype(ty) * 25 + S[j + 1] * 5 + S[k - 1];
-                const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? S[k - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
-                acc = fmaf(L.q5b[j] * L.Y[off(j - k, N) + k - 1], ct[CT_INVMM + cc] * e, acc);
+        float g0 = 0.f, g1 = 0.f;       // G column j for lanes m, 64 + m
+        if (N >= 5) {
+            const int cb = colb(N);
+            g0 = G[cb + min(lane, N - 5)];
+            g1 = G[cb + min(WAVE + lane, N - 5)];
+        }
+        for (int j = N; j >= 1; j--) {
+            float n0 = 0.f, n1 = 0.f;   // prefetch: column j - 1
+            if (j - 1 >= 5) {
+                const int cb = colb(j - 1);
+                n0 = G[cb + min(lane, j - 6)];
+                n1 = G[cb + min(WAVE + lane, j - 6)];
             }
-            const float val = nxt * sig1 + wave_sum_f(acc);
-            if (lane == 0) L.q5b[m] = val;
-            nxt = val;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (j >= 5) {
+                if (lane <= j - 5) acc0 = fmaf(val, g0, acc0);
+                if (WAVE + lane <= j - 5) acc1 = fmaf(val, g1, acc1);
+            }
+            // acc[j-5] is final now
+            const int m5 = j - 5;
+            float a5 = 0.f;
+            if (m5 >= 0)
+                a5 = __int_as_float(m5 < WAVE ? __builtin_amdgcn_readlane(__float_as_int(acc0), m5)
+                                              : __builtin_amdgcn_readlane(__float_as_int(acc1), m5 - WAVE));
+            val = fmaf(sig1, val, q0);   // q5b[j-1]
+            if (lane == 0) L.q5b[j - 1] = val;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = a5;
+            g0 = n0;
+            g1 = n1;
         }
     }
     // motif sites (unconstrained: the sequence alone decides)
@@ -315,154 +482,251 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         }
     }
     __syncthreads();
-    for (int k = tid; k < C; k += OX_NT) L.Y[k] = 0.f;
+    for (int k = tid; k < OX_WIN * L.RL; k += OX_NT) {
+        L.qw[k] = 0.f;
+        L.ow[k] = 0;
+    }
+    for (int k = tid; k < C; k += OX_NT) L.yc[k] = 0.f;
     __syncthreads();
 
+    OSTAMP(1);   // exterior adjoint + zeroing
     const float mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing, pw1 = XS->pwml[1];
     const float eTAU = XS->ctab[CT_FSM + 6];
 
-    // ---- the sweep: step d runs B and M of diagonal d and F of diagonal d + 1
-    for (int d = N - 1; d >= 3; d--) {
-        const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
-        const int par = d & 1;
-        if (wid < OX_NB) {
-            // ---------------- B: interior-loop gather of diagonal d (outer spans d+2 .. d+2+umax)
-            const int umax = min(30, N - 3 - d);
-            for (int ls = 0; ls < nls; ls++) {
-                int i = 1 + ls * WAVE + lane;
-                const bool valid = i <= N - d;
-                if (!valid) i = N - d;
-                const int j = i + d;
-                const int ty = ptype(S[i], S[j]);
-                const bool pr = valid && ty != 0;
-                float *pout = L.part + ((par * 2 + ls) * OX_NB + wid) * WAVE + lane;
-                if (umax < 0 || __ballot(pr) == 0) {   // no outer loop fits (or nothing pairs)
-                    *pout = 0.f;
-                    continue;
-                }
-                OxCell c;
-                c.i = i;
-                const int ty2 = rtype(ty);
-                const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
-                c.mmin = L.dt[DT_MMI + cc];
-                c.tau_in = ty2 > 2 ? eTAU : 1.f;
-                c.mo_in = ct[CT_ONEN + cc] * c.mmin;
-                c.m23_in = ct[CT_M23O + cc];
-                c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
-                if ((OX_TABLE_BLOCKS >> wid) & 1) {
-                    auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
-                    if (umax >= 2) {
-                        const int t1 = ptype(Sc(i - 2), Sc(j + 2));
-                        c.t11 = T.int11[t1][ty2][Sc(i - 1)][Sc(j + 1)];
-                    }
-                    if (umax >= 3) {
-                        const int ta = ptype(Sc(i - 2), Sc(j + 3)), tb = ptype(Sc(i - 3), Sc(j + 2));
-                        c.t12 = T.int21[ta][ty2][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
-                        c.t21 = T.int21[ty2][tb][Sc(j + 1)][Sc(i - 2)][Sc(i - 1)];
-                    }
-                    if (umax >= 4) {
-                        const int t1 = ptype(Sc(i - 3), Sc(j + 3));
-                        c.t22 = T.int22[t1][ty2][Sc(i - 2)][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
-                    }
-                }
-                float g = 0.f, sp = 0.f;
-                oblock(wid, L, XS, c, d, umax, ty2, g, sp);
-                *pout = fmaf(g, c.mmin, sp);
-            }
-        } else {
-            // ---------------- M: multiloop adjoint sums of diagonal d
-            const int mw = wid - OX_NB;                 // 0, 1: qmb; 2, 3: r2
-            const bool two = nls == 2;
-            const int ls = two ? (mw & 1) : 0;
-            if (d >= 4 && ls < nls) {
-                int i = 1 + ls * WAVE + lane;
-                const bool valid = i <= N - d;
-                if (!valid) i = N - d;
-                const int j = i + d;
-                float acc = 0.f;
-                if (mw < 2) {
-                    // qmb: t = 0 .. N-j-5, Y(i, j+5+t) = diag d+5+t, qm1(j+1, j+5+t) = diag 4+t
-                    const int lim = N - j - 5;
-                    const int tmax = N - (1 + ls * WAVE + d) - 5;           // lane-set's first cell
-                    const int h = two ? tmax + 1 : (tmax + 2) / 2;
-                    const int t0 = (two || mw == 0) ? 0 : h, t1 = two ? tmax + 1 : (mw == 0 ? h : tmax + 1);
-                    int ay = off(d + 5 + t0, N) + i - 1, aq = off(4 + t0, N) + j;
-                    for (int t = t0; t < t1; t++) {
-                        if (t <= lim) acc = fmaf(L.Y[ay], L.qm1[aq], acc);
-                        ay += N - (d + 5 + t);
-                        aq += N - (4 + t);
-                    }
-                } else {
-                    // r2: t = 5 .. i-1, Y(i-t, j) = diag d+t, qm(i-t, i-1) = diag t-1
-                    const int imax = min(N - d, (ls + 1) * WAVE);
-                    const int tmax = imax - 1;
-                    const int h = two ? tmax + 1 : (5 + tmax + 2) / 2;
-                    const int t0 = (two || mw == 2) ? 5 : h, t1 = two ? tmax + 1 : (mw == 2 ? h : tmax + 1);
-                    if (t0 < t1) {
-                        int ay = off(d + t0, N) + i - t0 - 1, aq = off(t0 - 1, N) + i - t0 - 1;
-                        for (int t = t0; t < t1; t++) {
-                            if (t <= i - 1) acc = fmaf(L.Y[ay], L.qm[aq], acc);
-                            ay += N - (d + t) - 1;
-                            aq += N - (t - 1) - 1;
-                        }
-                    }
-                }
-                L.mlp[(par * 4 + mw) * WAVE + lane] = acc;
-            }
-            // ---------------- F: finalize diagonal e = d + 1 (lane-set mw on wave 12 + mw)
-            const int e = d + 1;
-            const int nle = (N - e + WAVE - 1) / WAVE;
-            if (e <= N - 1 && mw < 2 && mw < nle) {
-                const int fl = mw;
-                const int pe = e & 1, pn = (e + 1) & 1;
-                const int i = 1 + fl * WAVE + lane;
-                if (i <= N - e) {
-                    const int j = i + e;
-                    const bool te = nle == 2;
-                    const float *mp = L.mlp + pe * 4 * WAVE;
-                    const float qmbv = te ? mp[fl * WAVE + lane] : mp[lane] + mp[WAVE + lane];
-                    const float r2 = te ? mp[(2 + fl) * WAVE + lane] : mp[2 * WAVE + lane] + mp[3 * WAVE + lane];
-                    const float R = i >= 2 ? pw1 * (L.rq[pn * NP + i - 1] + L.rr[pn * NP + i - 1]) : 0.f;
-                    const float chain = j < N ? mlbase_sig * L.r1[pn * NP + i] : 0.f;
-                    const float qm1b = qmbv + R + r2 + chain;
-                    L.rq[pe * NP + i] = qmbv;
-                    L.rr[pe * NP + i] = R;
-                    L.r1[pe * NP + i] = qm1b;
-                    const int ce = off(e, N) + i - 1;
-                    L.Y[ce] += qmbv;   // X(i, j) was stored two diagonals ago
-                    const int ty = ptype(S[i], S[j]);
-                    const int oc = ty * 25 + S[i + 1] * 5 + S[j - 1];
-                    float qbbm = 0.f;
-                    if (ty != 0) {
-                        float a_int = 0.f;
-                        const float *pp = L.part + (pe * 2 + fl) * OX_NB * WAVE + lane;
+    // Setup record of the cells of lane-set ls of diagonal D, written one step
+    // before B reads it: inner mismatch, TermAU, 1xn / 2x3 factors of the cell as
+    // the inner pair, the four 1x1..2x2 table factors (loaded from HBM one more
+    // step ahead, tab_load), type | pairable.
+    auto cell_of = [&](int D, int ls, int &i, int &j) {
+        i = 1 + ls * WAVE + lane;
+        const bool valid = i <= N - D;
+        if (!valid) i = N - D;
+        j = i + D;
+        return valid;
+    };
+    auto tab_load = [&](int D, int ls) {
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (D < 4 || ls >= (N - D + WAVE - 1) / WAVE) return t;
+        const int umax = min(30, N - 3 - D);
+        int i, j;
+        cell_of(D, ls, i, j);
+        const int ty2 = rtype(ptype(S[i], S[j]));
+        auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
+        if (umax >= 2) t.x = T.int11[ptype(Sc(i - 2), Sc(j + 2))][ty2][Sc(i - 1)][Sc(j + 1)];
+        if (umax >= 3) {
+            t.y = T.int21[ptype(Sc(i - 2), Sc(j + 3))][ty2][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
+            t.z = T.int21[ty2][ptype(Sc(i - 3), Sc(j + 2))][Sc(j + 1)][Sc(i - 2)][Sc(i - 1)];
+        }
+        if (umax >= 4) t.w = T.int22[ptype(Sc(i - 3), Sc(j + 3))][ty2][Sc(i - 2)][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
+        return t;
+    };
+    auto rec_write = [&](int D, int ls, float4 t) {
+        if (D < 4 || ls >= (N - D + WAVE - 1) / WAVE) return;
+        int i, j;
+        const bool valid = cell_of(D, ls, i, j);
+        const int ty = ptype(S[i], S[j]);
+        const int ty2 = rtype(ty);
+        const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
+        const float mmin = L.dt[DT_MMI + cc];
+        float *r = L.rec + (((D & 1) * 2 + ls) * OX_RF) * WAVE + lane;
+        r[0 * WAVE] = mmin;
+        r[1 * WAVE] = ty2 > 2 ? eTAU : 1.f;
+        r[2 * WAVE] = ct[CT_ONEN + cc] * mmin;
+        r[3 * WAVE] = ct[CT_M23O + cc];
+        r[4 * WAVE] = t.x;
+        r[5 * WAVE] = t.y;
+        r[6 * WAVE] = t.z;
+        r[7 * WAVE] = t.w;
+        r[8 * WAVE] = __int_as_float(ty2 | ((valid && ty != 0) ? 256 : 0));
+    };
+    constexpr int RW = 4;   // B waves RW, RW + 1: setup records of lane-sets 0, 1
+    float4 tnext = make_float4(0.f, 0.f, 0.f, 0.f);   // table factors of the diagonal after the next
+    if (wid == RW || wid == RW + 1) {
+        rec_write(N - 1, wid - RW, tab_load(N - 1, wid - RW));
+        tnext = tab_load(N - 2, wid - RW);
+    }
+    __syncthreads();
+
+    // Finalize record of lane-set ls of diagonal e (written at step e, read by F
+    // at step e - 1): the cell's exterior term q5b[j] q5[i-1] ext, multiloop stem,
+    // outer mismatch, multiloop-closing factor of the pair, type | code | pairable.
+    auto frec_write = [&](int e, int ls) {
+        if (e < 4 || ls >= (N - e + WAVE - 1) / WAVE) return;
+        int i, j;
+        const bool valid = cell_of(e, ls, i, j);
+        const int ty = ptype(S[i], S[j]);
+        const int oc = ty * 25 + S[i + 1] * 5 + S[j - 1];
+        float *r = L.fr + (((e & 1) * 2 + ls) * OX_FF) * WAVE + lane;
+        r[0] = L.q5b[j] * L.q5[i - 1] * L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
+        r[WAVE] = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
+        r[2 * WAVE] = L.dt[DT_MMI + oc];
+        r[3 * WAVE] = mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
+        r[4 * WAVE] = __int_as_float(ty | (oc << 8) | ((valid && ty != 0) ? (1 << 16) : 0));
+    };
+
+    // ---------------- F: finalize diagonal e = d + 1, lane-set fl (after the
+    // step's B work, on B waves 0 and 1): one batch of independent reads
+    auto finalize = [&](int d, int fl) {
+        const int e = d + 1;
+        const int nle = (N - e + WAVE - 1) / WAVE;
+        if (e > N - 1 || fl >= nle) return;
+        const int pe = e & 1, pn = (e + 1) & 1;
+        const int i = 1 + fl * WAVE + lane;
+        if (i > N - e) return;
+        const int j = i + e;
+        const bool te = nle == 2;
+        const float *mp = L.mlp + pe * OX_NM * WAVE + lane;
+        const float qmbv = te ? (fl ? mp[2 * WAVE] : mp[0] + mp[WAVE]) : mp[0] + mp[WAVE] + mp[2 * WAVE];
+        const float r2 = te ? (fl ? mp[4 * WAVE] + mp[5 * WAVE] : mp[3 * WAVE]) : mp[3 * WAVE] + mp[4 * WAVE] + mp[5 * WAVE];
+        const float R = i >= 2 ? pw1 * (L.rq[pn * NP + i - 1] + L.rr[pn * NP + i - 1]) : 0.f;
+        const float chain = j < N ? mlbase_sig * L.r1[pn * NP + i] : 0.f;
+        const float qm1b = qmbv + R + r2 + chain;
+        const float *fr = L.fr + ((pe * 2 + fl) * OX_FF) * WAVE + lane;
+        const int tp = __float_as_int(fr[4 * WAVE]);
+        float a_int = 0.f;
+        const float *pp = L.part + (pe * 2 + fl) * OX_NB * WAVE + lane;
 #pragma unroll
-                        for (int b = 0; b < OX_NB; b++) a_int += pp[b * WAVE];
-                        const float ext = L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
-                        const float stem = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
-                        const float qbb = a_int + L.q5b[j] * L.q5[i - 1] * ext + qm1b * stem;
-                        qbbm = qbb * L.dt[DT_MMI + oc];
-                        if (e - 2 >= 4)   // X(i+1, j-1): this pair closing a multiloop
-                            L.Y[off(e - 2, N) + i] =
-                                qbb * mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
-                        if (motif && e == mL - 1 && L.mat[i])
-                            L.pm[i] = float(double(qbb) * XS->motif_extra / Z);
-                        for (int t = 0; t < ka.n_pairs && t < OX_MAXP; t++) {
-                            if (ka.pairs[3 * t] == bv && ka.pairs[3 * t + 1] == i && ka.pairs[3 * t + 2] == j) {
-                                const int cc = rtype(ty) * 25 + S[j + 1] * 5 + S[i - 1];
-                                const double qb = double(src[ce]) * double(ct[CT_INVMM + cc]);
-                                L.pd[t] = qb * double(qbb) / double(Z);
-                            }
-                        }
-                    }
-                    const int wo = wslot(e) * L.RL + OX_PAD + i - 1;
-                    L.qw[wo] = qbbm;
-                    L.ow[wo] = uint8_t(oc);
+        for (int b = 0; b < OX_NB; b++) a_int += pp[b * WAVE];
+        L.rq[pe * NP + i] = qmbv;
+        L.rr[pe * NP + i] = R;
+        L.r1[pe * NP + i] = qm1b;
+        L.yr[rowb(i, N) + e - 4] += qmbv;   // Y(i, j): X(i, j) was stored two diagonals ago
+        L.yc[colb(j) + i - 1] += qmbv;
+        float qbbm = 0.f;
+        if (tp >> 16) {
+            const float qbb = a_int + fr[0] + qm1b * fr[WAVE];
+            qbbm = qbb * fr[2 * WAVE];
+            if (e - 2 >= 4) {   // X(i+1, j-1): this pair closing a multiloop
+                const float x = qbb * fr[3 * WAVE];
+                L.yr[rowb(i + 1, N) + e - 6] = x;
+                L.yc[colb(j - 1) + i] = x;
+            }
+            if (motif && e == mL - 1 && L.mat[i]) L.pm[i] = float(double(qbb) * XS->motif_extra / Z);
+            const int npl = L.pl[OX_MAXP];
+            for (int q = 0; q < npl; q++) {
+                const int pk = L.pl[q];
+                if (((pk >> 8) & 255) == i && (pk >> 16) == j) {
+                    const int cc = rtype(tp & 255) * 25 + S[j + 1] * 5 + S[i - 1];
+                    const double qb = double(src[off(e, N) + i - 1]) * double(ct[CT_INVMM + cc]);
+                    L.pd[pk & 255] = qb * double(qbb) / double(Z);
                 }
             }
         }
+        const int wo = wslot(e) * L.RL + OX_PAD + i - 1;
+        L.qw[wo] = qbbm;
+        L.ow[wo] = uint8_t((tp >> 8) & 255);
+    };
+    auto fin = [&](int d) {
+        if (wid < 2) {
+            finalize(d, wid);
+        } else if (wid < 4) {
+            frec_write(d, wid - 2);   // diagonal d, finalized next step
+        } else if (wid < RW + 2) {
+            // setup records of diagonal d - 1 (next step's B), with the table factors
+            // loaded last step; the loads for diagonal d - 2
+            rec_write(d - 1, wid - RW, tnext);
+            tnext = tab_load(d - 2, wid - RW);
+        }
+    };
+
+    // ---- the sweep: step d runs B and M of diagonal d and F of diagonal d + 1.
+    // B: loop sizes in blocks of about equal cost (generic shape ~2 instructions,
+    // a special ~9); the 1x1..2x2 table shapes (u = 2, 3, 4) last in their blocks
+    if (wid < OX_NB) {
+        switch (wid) {
+            case 0: b_sweep<30, 12, 1, 0>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 1: b_sweep<29, 11, 5, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 2: b_sweep<28, 13, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 3: b_sweep<27, 14, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 4: b_sweep<26, 15, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 5: b_sweep<25, 16, 4, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 6: b_sweep<24, 17, 7, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 7: b_sweep<23, 18, 6, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 8: b_sweep<22, 19, 3, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            default: b_sweep<21, 20, 2, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+        }
+    } else for (int d = N - 1; d >= 3; d--) {
+        const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
+        const int par = d & 1;
+        {
+            // ---------------- M: multiloop adjoint sums of diagonal d.  Work items:
+            // two lane-sets: qmb ls0 (halves on waves 0, 1), qmb ls1, r2 ls0, r2 ls1
+            // (halves on 4, 5); one lane-set: qmb and r2 in thirds
+            const int mw = wid - OX_NB;
+            if (d >= 4) {
+                const bool two = nls == 2;
+                const bool isq = mw < 3;
+                const int ls = two ? ((mw == 2 || mw >= 4) ? 1 : 0) : 0;
+                const int np = two ? ((mw <= 1 || mw >= 4) ? 2 : 1) : 3;                 // parts of the item
+                const int pi = two ? (mw == 1 || mw == 5 ? 1 : 0) : (mw % 3);            // this wave's part
+                int i = 1 + ls * WAVE + lane;
+                const int ilast = min(N - d, (ls + 1) * WAVE);
+                const bool valid = i <= N - d;
+                if (!valid) i = N - d;
+                const int j = i + d;
+                float acc = 0.f, acc1 = 0.f;
+                if (isq) {
+                    // qmb: t = 0 .. N-j-5: Y(i, j+5+t) = YR[rowb(i) + d + 1 + t],
+                    // qm1(j+1, j+5+t) = Q1R[rowb(j+1) + t]
+                    const int lim = N - j - 5;
+                    const int T = N - (1 + ls * WAVE + d) - 4;          // the lane-set's longest range
+                    const int ta = (T * pi) / np, tb = (T * (pi + 1)) / np;
+                    const float *py = L.yr + rowb(i, N) + d + 1, *pq = L.q1r + rowb(j + 1, N);
+                    for (int t = ta; t < tb; t += 16) {
+                        float yv[16], qv[16];
+#pragma unroll
+                        for (int k = 0; k < 16; k++) { yv[k] = py[t + k]; qv[k] = pq[t + k]; }
+                        if (__ballot(lim < t + 15 || tb < t + 16) == 0) {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                acc = fmaf(yv[k], qv[k], acc);
+                                acc1 = fmaf(yv[k + 1], qv[k + 1], acc1);
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, qv[k], acc);
+                                acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, qv[k + 1], acc1);
+                            }
+                        }
+                    }
+                } else {
+                    // r2: ip = 1 .. i-5: Y(ip, j) = YC[colb(j) + ip - 1], qm(ip, i-1) = QMC[colb(i-1) + ip - 1]
+                    const int lim = i - 5;
+                    const int T = ilast - 5;
+                    const int ta = 1 + (T * pi) / np, tb = 1 + (T * (pi + 1)) / np;
+                    const float *py = L.yc + colb(j) - 1, *pq = L.qmc + colb(i - 1) - 1;
+                    for (int t = ta; t < tb; t += 16) {
+                        float yv[16], qv[16];
+#pragma unroll
+                        for (int k = 0; k < 16; k++) { yv[k] = py[t + k]; qv[k] = pq[t + k]; }
+                        if (__ballot(lim < t + 15 || tb < t + 16) == 0) {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                acc = fmaf(yv[k], qv[k], acc);
+                                acc1 = fmaf(yv[k + 1], qv[k + 1], acc1);
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, qv[k], acc);
+                                acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, qv[k + 1], acc1);
+                            }
+                        }
+                    }
+                }
+                L.mlp[(par * OX_NM + mw) * WAVE + lane] = acc + acc1;
+            }
+            OSTAMP(4);   // M sums
+        }
+        OSTAMP(5);   // F (M waves) / B tail
         lds_barrier();
+        OSTAMP(6);   // barrier
     }
+#ifdef ADX_STAMP
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_stamps_o[wid][k], st_acc[k]);
+#endif
     // ---- requested pairs of this fold (score terms), the motif's inner pairs credited
     // from its closing cell (kernels.hip outside())
     double *pp = pair_p + size_t(w) * ka.n_pairs;
@@ -490,8 +754,8 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
 // LDS bytes of the lanes = cells outside kernel for this workload (0: not covered)
 size_t outside_cells_lds(const KArgs &ka) {
     if (ka.Nmax > OX_NMAX || ka.Nmax < 8 || ka.n_pairs > OX_MAXP || !ka.tab) return 0;
-    const size_t b = OxLay(ka.Nmax).BYTES;
-    return b + 256 <= 160 * 1024 ? b : 0;
+    const OxLay y(ka.Nmax);
+    return y.BYTES + 256 <= 160 * 1024 ? y.BYTES : 0;
 }
 
 hipError_t launch_outside_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *pair_p,
@@ -511,3 +775,14 @@ hipError_t launch_outside_cells(const KArgs &ka, const uint8_t *seqs, int W, con
 }
 
 }  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps_outside(unsigned long long *out, int reset) {  // [16][8]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_o), sizeof(adx::g_stamps_o)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_o), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif
