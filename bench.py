@@ -266,7 +266,9 @@ def main():
     state_bytes = 2 * (1 if a.fold == "mfe" else 2) * (3 * cells + a.length + 2) * 4
     traffic, traffic_src = None, None
     if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_latest_%s.json" % a.fold)
+        # the PMC summary of this exact workload (fold, pair terms, length), else null
+        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_latest_%s%s%s.json" % (
+            a.fold, "_bppm" if a.bppm else "", "" if a.length == 100 else "_n%d" % a.length))
     if a.traffic_json and os.path.exists(a.traffic_json):
         with open(a.traffic_json) as f:
             tj = json.load(f)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# HBM traffic per step (FETCH_SIZE / WRITE_SIZE, one counter per rocprofv3
+# pass, MI355X_MICROARCH.md HBM corrections in tools/pmc_traffic.py) of the
+# bench workloads: mfe, pf, pf + bppm at N = 100 and 150.
+# usage: tools/gpu_traffic.sh <tag>   -> gpurun_out/<tag>/traffic_latest_*.json
+set -e
+tag=${1:-traffic}
+D=gpurun_out/$tag
+mkdir -p $D
+export TMPDIR=/tmp
+run() {   # name, bench args
+  local n=$1; shift
+  timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $D/$n/f -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $D/$n.fetch.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $D/$n/w -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $D/$n.write.log 2>&1
+  python tools/pmc_traffic.py $(find $D/$n/f -name "*counter_collection.csv") $(find $D/$n/w -name "*counter_collection.csv") > $D/traffic_latest_$n.json
+}
+run mfe
+run pf --fold pf
+run pf_bppm --bppm
+run pf_bppm_n150 --bppm --length 150

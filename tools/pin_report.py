@@ -3,7 +3,7 @@
 
 The five RNAfold annotations (test_scoring.cc:52-55, 86-87, 152-154) and the
 macrostate / base-pair-probability thresholds (test_scoring.cc:83-259), for
-a parameter file (default: the shipped one) and a motif mode (REPLACE = 1).
+a parameter file (default: the shipped one) and a motif mode (default AUTO = 2: ADD in partition functions, REPLACE in the MFE).
 
 Usage: python tools/pin_report.py [params.par] [motif_mode]
 """
@@ -21,7 +21,7 @@ HAIRPIN = "ACGUGAAAACGU"
 
 def main():
     par = sys.argv[1] if len(sys.argv) > 1 else O.DEFAULT_PAR
-    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     P = O.Params(par)
     theo = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), mode)
     rhf = workloads.RHF6_SEQ.upper()

@@ -15,8 +15,9 @@ import csv
 import json
 import sys
 
-# the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip)
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel")
+# the kernels of one step's score window (kernels.hip, mfe_cells.hip, outside_cells.hip):
+# the fold kernels, and with pair terms the outside pass and the score combine
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "outside_cells_kernel", "bppm_kernel", "combine_kernel")
 
 
 def per_kernel(path, counter):
