@@ -61,12 +61,12 @@ constexpr int OX_MAXP = 64;           // requested pairs of one fold kept in LDS
 constexpr int OX_NMAX = 112;
 constexpr int OX_SLACK = 64;          // zeroed floats after each cell table (reads past a row end)
 constexpr int OX_FF = 5;              // finalize record fields (see frec_write)
-constexpr int OX_RF = 9;              // cell setup record fields (see rec_write)
+constexpr int OX_RF = 10;             // cell setup record fields (see rec_write)
 
 // LDS carve for folded length N (runtime; the host sizes the launch with it)
 struct OxLay {
     int C, NP, RL;
-    size_t YR, YC, Q1R, QMC, QW, OW, PART, MLP, REC, FR, SF, RQ, RR, R1, Q5, Q5B, PM, CT, DT, PD, PL, S, MT, BYTES;
+    size_t YR, YC, Q1R, QMC, QW, OW, PART, MLP, REC, CL, FR, SF, RQ, RR, R1, Q5, Q5B, PM, CT, DT, PD, PL, S, MT, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit OxLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
@@ -82,7 +82,8 @@ struct OxLay {
         OW = o;   o += a16(size_t(OX_WIN) * RL);                 // outer codes window
         PART = o; o += a16(size_t(2) * 2 * OX_NB * WAVE * 4);   // [parity][lane-set][block][lane]
         MLP = o;  o += a16(size_t(2) * OX_NM * WAVE * 4);       // [parity][M wave][lane]
-        REC = o;  o += a16(size_t(2) * 2 * OX_RF * WAVE * 4);   // cell setup records [parity][lane-set][field][lane]
+        REC = o;  o += a16(size_t(2) * 2 * OX_RF * WAVE * 4 + 16);   // cell setup records [parity][lane-set][field][lane]; counts [parity]
+        CL = o;   o += a16(size_t(2) * 2 * WAVE);                // compacted pairable cells [parity][slot]
         FR = o;   o += a16(size_t(2) * 2 * OX_FF * WAVE * 4);   // finalize records [parity][lane-set][field][lane]
         SF = o;   o += a16(size_t(31) * 32 * 4);                 // constant factor of shape (u, n1): [u][n1]
         RQ = o;   o += a16(size_t(2) * NP * 4);                  // qmb ring [parity][i]
@@ -104,7 +105,8 @@ struct OxLay {
 struct OxL {
     float *yr, *yc, *q1r, *qmc, *qw, *part, *mlp, *rec, *fr, *sf, *rq, *rr, *r1, *q5, *q5b, *pm, *ct, *dt;
     int *pl;
-    uint8_t *ow, *S, *mat;
+    uint8_t *ow, *S, *mat, *cl;
+    int *rcnt;
     double *pd;
     int RL, NP;
 };
@@ -227,19 +229,14 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
     s2.load(L);
     s3.load(L);
     for (int d = N - 1; d >= 3; d--) {
-        const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
         const int par = d & 1;
         const int umax = min(30, N - 3 - d);                      // outer spans d+2 .. d+2+umax
-        for (int ls = 0; ls < nls; ls++) {
-            int i = 1 + ls * WAVE + lane;
-            if (i > N - d) i = N - d;
+        // lanes = the pairable cells of diagonal d, compacted (records one step ahead)
+        const int ncls = (d >= 4 && umax >= 0) ? (uni(L.rcnt[par]) + WAVE - 1) / WAVE : 0;
+        for (int ls = 0; ls < ncls; ls++) {
             const float *r = L.rec + ((par * 2 + ls) * OX_RF) * WAVE + lane;
             const int tp = __float_as_int(r[8 * WAVE]);
-            float *pout = L.part + ((par * 2 + ls) * OX_NB + wid) * WAVE + lane;
-            if (umax < 0 || __ballot(tp >= 256) == 0) {   // no outer loop fits (or nothing pairs)
-                *pout = 0.f;
-                continue;
-            }
+            const int i = __float_as_int(r[9 * WAVE]);
             OxCell c;
             c.i = i;
             const int ty2 = tp & 255;
@@ -261,7 +258,8 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
             s2.run(L, c, d, umax, ty2, g, sp);
             s3.run(L, c, d, umax, ty2, g, sp);
             OSTAMP(3);   // B shapes
-            *pout = fmaf(g, c.mmin, sp);
+            if (tp >= 256)   // the cell's natural slot (F reads lane = cell)
+                L.part[((par * 2 + ((i - 1) >> 6)) * OX_NB + wid) * WAVE + ((i - 1) & (WAVE - 1))] = fmaf(g, c.mmin, sp);
         }
         fin(d);   // F of diagonal d + 1 on waves 0 and 1
         OSTAMP(5);
@@ -299,6 +297,8 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     L.part = reinterpret_cast<float *>(smem + Y.PART);
     L.mlp = reinterpret_cast<float *>(smem + Y.MLP);
     L.rec = reinterpret_cast<float *>(smem + Y.REC);
+    L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(2) * 2 * OX_RF * WAVE * 4);
+    L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);
     L.sf = reinterpret_cast<float *>(smem + Y.SF);
     L.fr = reinterpret_cast<float *>(smem + Y.FR);
     L.rq = reinterpret_cast<float *>(smem + Y.RQ);
@@ -504,46 +504,86 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         j = i + D;
         return valid;
     };
-    auto tab_load = [&](int D, int ls) {
-        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (D < 4 || ls >= (N - D + WAVE - 1) / WAVE) return t;
+    // The pairable cells of diagonal D are compacted (ballot + mbcnt over the
+    // natural lane-sets, one wave): compacted lane-set k holds cells
+    // ci[k] (0: none), whose table factors t[k] are loaded one step before the
+    // record is written.
+    struct Pend {
+        int ci[2];
+        float4 t[2];
+        int cnt;
+    };
+    auto tab_load = [&](int D) {
+        Pend P;
+        P.ci[0] = P.ci[1] = 0;
+        P.t[0] = P.t[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        P.cnt = 0;
+        if (D < 4) return P;
         const int umax = min(30, N - 3 - D);
-        int i, j;
-        cell_of(D, ls, i, j);
-        const int ty2 = rtype(ptype(S[i], S[j]));
-        auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
-        if (umax >= 2) t.x = T.int11[ptype(Sc(i - 2), Sc(j + 2))][ty2][Sc(i - 1)][Sc(j + 1)];
-        if (umax >= 3) {
-            t.y = T.int21[ptype(Sc(i - 2), Sc(j + 3))][ty2][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
-            t.z = T.int21[ty2][ptype(Sc(i - 3), Sc(j + 2))][Sc(j + 1)][Sc(i - 2)][Sc(i - 1)];
+        const int nls = (N - D + WAVE - 1) / WAVE;
+        int base = 0;
+        for (int ls = 0; ls < nls; ls++) {
+            const int i = 1 + ls * WAVE + lane;
+            const bool pr = i <= N - D && ptype(S[i], S[i + D]) != 0;
+            const uint64_t m = __ballot(pr);
+            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            if (pr) L.cl[(D & 1) * 2 * WAVE + slot] = uint8_t(i);
+            base += __popcll(m);
         }
-        if (umax >= 4) t.w = T.int22[ptype(Sc(i - 3), Sc(j + 3))][ty2][Sc(i - 2)][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
-        return t;
+        P.cnt = base;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
+        for (int k = 0; k < 2; k++) {
+            const int idx = k * WAVE + lane;
+            if (idx >= base) continue;
+            const int i = L.cl[(D & 1) * 2 * WAVE + idx], j = i + D;
+            P.ci[k] = i;
+            const int ty2 = rtype(ptype(S[i], S[j]));
+            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (umax >= 2) t.x = T.int11[ptype(Sc(i - 2), Sc(j + 2))][ty2][Sc(i - 1)][Sc(j + 1)];
+            if (umax >= 3) {
+                t.y = T.int21[ptype(Sc(i - 2), Sc(j + 3))][ty2][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
+                t.z = T.int21[ty2][ptype(Sc(i - 3), Sc(j + 2))][Sc(j + 1)][Sc(i - 2)][Sc(i - 1)];
+            }
+            if (umax >= 4) t.w = T.int22[ptype(Sc(i - 3), Sc(j + 3))][ty2][Sc(i - 2)][Sc(i - 1)][Sc(j + 1)][Sc(j + 2)];
+            P.t[k] = t;
+        }
+        return P;
     };
-    auto rec_write = [&](int D, int ls, float4 t) {
-        if (D < 4 || ls >= (N - D + WAVE - 1) / WAVE) return;
-        int i, j;
-        const bool valid = cell_of(D, ls, i, j);
-        const int ty = ptype(S[i], S[j]);
-        const int ty2 = rtype(ty);
-        const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
-        const float mmin = L.dt[DT_MMI + cc];
-        float *r = L.rec + (((D & 1) * 2 + ls) * OX_RF) * WAVE + lane;
-        r[0 * WAVE] = mmin;
-        r[1 * WAVE] = ty2 > 2 ? eTAU : 1.f;
-        r[2 * WAVE] = ct[CT_ONEN + cc] * mmin;
-        r[3 * WAVE] = ct[CT_M23O + cc];
-        r[4 * WAVE] = t.x;
-        r[5 * WAVE] = t.y;
-        r[6 * WAVE] = t.z;
-        r[7 * WAVE] = t.w;
-        r[8 * WAVE] = __int_as_float(ty2 | ((valid && ty != 0) ? 256 : 0));
+    // records of diagonal D's compacted pairable cells (read by B at step D)
+    auto rec_write = [&](int D, const Pend &P) {
+        if (D < 4) return;
+        if (lane == 0) L.rcnt[D & 1] = P.cnt;
+        for (int k = 0; k < 2; k++) {
+            const int idx = k * WAVE + lane;
+            if (k * WAVE >= P.cnt) break;
+            const bool v = idx < P.cnt;
+            const int i = v ? P.ci[k] : 1, j = i + D;
+            const int ty2 = rtype(ptype(S[i], S[j]));
+            const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
+            const float mmin = L.dt[DT_MMI + cc];
+            float *r = L.rec + (((D & 1) * 2 + k) * OX_RF) * WAVE + lane;
+            r[0 * WAVE] = mmin;
+            r[1 * WAVE] = ty2 > 2 ? eTAU : 1.f;
+            r[2 * WAVE] = ct[CT_ONEN + cc] * mmin;
+            r[3 * WAVE] = ct[CT_M23O + cc];
+            r[4 * WAVE] = P.t[k].x;
+            r[5 * WAVE] = P.t[k].y;
+            r[6 * WAVE] = P.t[k].z;
+            r[7 * WAVE] = P.t[k].w;
+            r[8 * WAVE] = __int_as_float(ty2 | (v ? 256 : 0));
+            r[9 * WAVE] = __int_as_float(i);   // an idle lane reads cell 1's shapes (discarded)
+        }
     };
-    constexpr int RW = 4;   // B waves RW, RW + 1: setup records of lane-sets 0, 1
-    float4 tnext = make_float4(0.f, 0.f, 0.f, 0.f);   // table factors of the diagonal after the next
-    if (wid == RW || wid == RW + 1) {
-        rec_write(N - 1, wid - RW, tab_load(N - 1, wid - RW));
-        tnext = tab_load(N - 2, wid - RW);
+    constexpr int RW = 7;   // B wave RW: setup records (both lane-sets)
+    Pend pnext;             // compaction + table factors of the diagonal after the next
+    pnext.ci[0] = pnext.ci[1] = 0;
+    pnext.cnt = 0;
+    if (wid == RW) {
+        rec_write(N - 1, tab_load(N - 1));
+        pnext = tab_load(N - 2);
     }
     __syncthreads();
 
@@ -583,10 +623,11 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         const float qm1b = qmbv + R + r2 + chain;
         const float *fr = L.fr + ((pe * 2 + fl) * OX_FF) * WAVE + lane;
         const int tp = __float_as_int(fr[4 * WAVE]);
-        float a_int = 0.f;
+        float a_int = 0.f;   // B wrote the partials of every pairable cell when an outer loop fits
         const float *pp = L.part + (pe * 2 + fl) * OX_NB * WAVE + lane;
 #pragma unroll
         for (int b = 0; b < OX_NB; b++) a_int += pp[b * WAVE];
+        if (N - 3 - e < 0) a_int = 0.f;
         L.rq[pe * NP + i] = qmbv;
         L.rr[pe * NP + i] = R;
         L.r1[pe * NP + i] = qm1b;
@@ -621,11 +662,11 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             finalize(d, wid);
         } else if (wid < 4) {
             frec_write(d, wid - 2);   // diagonal d, finalized next step
-        } else if (wid < RW + 2) {
-            // setup records of diagonal d - 1 (next step's B), with the table factors
-            // loaded last step; the loads for diagonal d - 2
-            rec_write(d - 1, wid - RW, tnext);
-            tnext = tab_load(d - 2, wid - RW);
+        } else if (wid == RW) {
+            // setup records of diagonal d - 1 (next step's B), with the compaction and
+            // table factors made last step; those of diagonal d - 2
+            rec_write(d - 1, pnext);
+            pnext = tab_load(d - 2);
         }
     };
 
