@@ -431,7 +431,8 @@ struct Problem {
     bool mfe_cells_ok = false;   // Ninio saturated from |n1-n2| = 5 on, MLbase >= 0 (mfe_cells.hip)
     // incremental-fold state of the MC walkers (kernels.hip Inc)
     DevBuf<float> dTab;
-    DevBuf<float> dGstep;        // [W][n_variants] (pair terms: score before the outside pass)
+    DevBuf<float> dGstep;        // [W][n_variants] energies of the step's folds (pf_cells_kernel,
+                                 //   and the pair-term score that waits for the outside pass)
     DevBuf<uint8_t> dCur, dValid;
     DevBuf<int> dChg;
     size_t tab_slot = 0;
@@ -494,7 +495,7 @@ struct Problem {
         ka.cur_slot = st ? dCur.p : nullptr;
         ka.tab_valid = st ? dValid.p : nullptr;
         ka.chg = st ? dChg.p : nullptr;
-        ka.gstep = st && !pairs.empty() ? dGstep.p : nullptr;
+        ka.gstep = dGstep.p;
         return ka;
     }
 
@@ -560,7 +561,7 @@ struct Problem {
         HIP_TRY(dCur.alloc(W));
         HIP_TRY(dValid.alloc(W));
         HIP_TRY(dChg.alloc(size_t(W) * 2));
-        if (!pairs.empty()) HIP_TRY(dGstep.alloc(size_t(W) * variants.size()));
+        if (adx_status sg = ensure_gstep(W)) return sg;
         HIP_TRY(hipMemsetAsync(dCur.p, 1, W, stream));     // the initial fold writes slot 0
         HIP_TRY(hipMemsetAsync(dValid.p, 0, W, stream));
         HIP_TRY(hipMemsetAsync(dChg.p, 0xff, sizeof(int) * 2 * W, stream));
@@ -628,9 +629,17 @@ struct Problem {
         return ADX_OK;
     }
 
+    adx_status ensure_gstep(int W) {
+        const size_t need = size_t(W) * variants.size();
+        if (dGstep.n < need) HIP_TRY(dGstep.alloc(need));
+        return ADX_OK;
+    }
+
     // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
     adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
         adx_status so = ensure_ovf(W);
+        if (so) return so;
+        so = ensure_gstep(W);
         if (so) return so;
         if (!pairs.empty()) {
             adx_status s = ensure_pairs(W);
@@ -771,7 +780,7 @@ static adx_status fold_energy(adx_fold *f, int mode, float *energy, std::vector<
         if (s) return s;
         HIP_TRY(hipMemcpyAsync(&g, ddg.p, sizeof(float), hipMemcpyDeviceToHost, pb.stream));
         HIP_TRY(hipStreamSynchronize(pb.stream));
-        if (std::isfinite(g) || std::isinf(g) && g > 0) {
+        if (std::isfinite(g) || (std::isinf(g) && g > 0)) {
             // +inf = empty (constrained) ensemble; recalibrate once for accuracy
             if (attempt == 0 && std::isfinite(g) && N > 0) {
                 pb.g0 = std::min(-0.05, static_cast<double>(g) / N);

@@ -1889,7 +1889,37 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
     return hipGetLastError();
 }
 
+// Scores from the per-variant energies a fold kernel left in KArgs::gstep
+// (combine_score, one thread per walker): after pf_cells_kernel, and after the
+// outside pass once it has written the pair probabilities (pair_p null: the
+// pair terms read 0.5, as combine_score).
+__global__ void combine_kernel(KArgs ka, int W, const int *mask, double *scores, double *terms) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W || (mask && mask[w] != 1)) return;
+    const float *g = ka.gstep + size_t(w) * ka.n_variants;
+    const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
+    const int nt = ka.n_terms * ka.n_ctx_eff;
+    double *tv = terms ? terms + size_t(w) * nt : nullptr;
+    const DevScaled &X = *ka.X;
+    double score = 0.0;
+    for (int c = 0; c < ka.n_ctx_eff; c++) {
+        for (int t = 0; t < ka.n_terms; t++) {
+            const DevTermMap m = ka.tmap[c * ka.n_terms + t];
+            double p = (m.kind == 1) ? (pp ? pp[m.pidx] : 0.5)
+                                     : exp((static_cast<double>(g[m.vfree]) - static_cast<double>(g[m.vcons])) / X.kT);
+            if (!m.favorable) p = 1.0 - p;
+            const double val = log(p);
+            if (tv) tv[c * ka.n_terms + t] = val;
+            score += m.weight * val;
+        }
+    }
+    scores[w] = score;
+}
+
 size_t mfe_cells_lds(const KArgs &ka);
+size_t pf_cells_lds(const KArgs &ka);
+hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
+                           hipStream_t stream);
 hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
                             const int *mask, hipStream_t stream);
 
@@ -1900,6 +1930,10 @@ hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double 
 // kernel does not cover (mfe_cells_lds() == 0)
 static bool mfe_rows_forced() {
     const char *e = std::getenv("ADX_MFE_KERNEL");
+    return e && std::strcmp(e, "rows") == 0;
+}
+static bool pf_rows_forced() {
+    const char *e = std::getenv("ADX_PF_KERNEL");
     return e && std::strcmp(e, "rows") == 0;
 }
 
@@ -1926,6 +1960,18 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         if (choose_p(ka) == 2)
             return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
         return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+    }
+    // partition functions: pf_cells_kernel (lanes = cells, pf_cells.hip) where it
+    // covers the length, energies to dG (or the gstep scratch), then the scores;
+    // else score_kernel<SumProd> (lanes = terms).  ADX_PF_KERNEL=rows forces the latter.
+    float *g = dG ? dG : ka.gstep;
+    if (g && !pf_rows_forced() && choose_p(ka) == 2 && ka.n_groups2 > 0 && pf_cells_lds(ka) > 0) {
+        hipError_t e = launch_pf_cells(ka, seqs, W, mask, g, stream);
+        if (e != hipSuccess) return e;
+        KArgs kc = ka;
+        kc.gstep = g;
+        hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
+        return hipGetLastError();
     }
     if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
     return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
@@ -1989,32 +2035,6 @@ hipError_t launch_outside_cells(const KArgs &ka, const uint8_t *seqs, int W, con
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
                        double *pair_p, char *scratch, hipStream_t stream) {
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
-}
-
-// Scores of the step's proposals once the outside pass has written the pair
-// probabilities: combine_score over the per-variant energies score_kernel left
-// in KArgs::gstep (one thread per walker).
-__global__ void combine_kernel(KArgs ka, int W, const int *mask, double *scores, double *terms) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W || (mask && mask[w] != 1)) return;
-    const float *g = ka.gstep + size_t(w) * ka.n_variants;
-    const double *pp = ka.pair_p + size_t(w) * ka.n_pairs;
-    const int nt = ka.n_terms * ka.n_ctx_eff;
-    double *tv = terms ? terms + size_t(w) * nt : nullptr;
-    const DevScaled &X = *ka.X;
-    double score = 0.0;
-    for (int c = 0; c < ka.n_ctx_eff; c++) {
-        for (int t = 0; t < ka.n_terms; t++) {
-            const DevTermMap m = ka.tmap[c * ka.n_terms + t];
-            double p = (m.kind == 1) ? pp[m.pidx]
-                                     : exp((static_cast<double>(g[m.vfree]) - static_cast<double>(g[m.vcons])) / X.kT);
-            if (!m.favorable) p = 1.0 - p;
-            const double val = log(p);
-            if (tv) tv[c * ka.n_terms + t] = val;
-            score += m.weight * val;
-        }
-    }
-    scores[w] = score;
 }
 
 // evs (optional): 2 * nsteps events recorded around each step's score launch

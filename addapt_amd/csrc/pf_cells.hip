@@ -1,0 +1,727 @@
+// gfx950 McCaskill inside pass (the reference's scoring path, vrna_pf at
+// scoring.cc:58,65; BASELINE configs 3-5 and the PF bench) with lanes = cells
+// -- the same recursions, constraints, ligand motif and incremental folds as
+// kernels.hip pf_group<…, 2, SumProd> (oracle/fold.c orc_pf_energy), mapped
+// the way outside_cells.hip maps the outside pass:
+//
+//   * one workgroup (14 waves) per (walker, group of the apo and holo
+//     variants of one (context, macrostate)), the two folds in lockstep as
+//     float2 (ds_read_b64, v_pk_fma_f32: one instruction serves both);
+//   * one anti-diagonal per step, ONE barrier per step.  Step s runs
+//       B   the interior-loop sums of diagonal s (waves 0-7, lanes = the
+//           changed pairable cells compacted one step ahead; shapes by loop
+//           size in blocks of equal cost, factors in registers; every shape
+//           one read of the inner cell at a per-lane base plus an immediate
+//           offset);
+//       M   the qm (fML) items of span s-2 (waves 8-10; K lanes per item so
+//           that the few long items of late spans spread over the waves, the
+//           split points read from the row-major qm and column-major qm1 at
+//           immediate offsets);
+//       F   the cells of diagonal s-1 (wave 11): qb, qbm, qm1;
+//       Q   q5[s-1] (wave 12);
+//       R   the compaction and setup records of diagonal s+1 (wave 13).
+//
+// Covered: N <= 100 (LDS); longer folds take kernels.hip score_kernel.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "dev_types.hpp"
+#include "fold_common.hpp"
+
+namespace adx {
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int PX_NW = 14;
+constexpr int PX_NT = PX_NW * WAVE;
+constexpr int PX_NB = 8;              // interior-loop blocks (waves 0..7)
+constexpr int PX_NMW = 3;             // qm item waves (8..10); then F (11), Q (12), records (13)
+constexpr int PX_NMAX = 100;
+constexpr int PX_RF = 10;             // record fields (rec_write)
+constexpr int PX_SLACK = 16;
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 sp2(float x) { return f2{x, x}; }
+__device__ __forceinline__ bool is_mark2(f2 v) { return __float_as_uint(v.x) == 0x80000000u; }
+
+struct PxLay {
+    int C, NP;
+    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, Q5, CT, DT, PW, BY, BYTES;
+    __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
+    __host__ __device__ explicit PxLay(int N) {
+        C = ((N - 4) * (N - 3)) / 2;
+        NP = N + 2;
+        size_t o = 0;
+        QB = o;   o += a16((size_t(C) + PX_SLACK) * 8);           // qb * mismatchI(inner), diagonal-major
+        QM = o;   o += a16((size_t(C) + PX_SLACK) * 8);           // qm, row-major
+        Q1 = o;   o += a16((size_t(C) + PX_SLACK) * 8);           // qm1, column-major
+        CC = o;   o += a16(size_t(C) + PX_SLACK);                 // inner-pair code per cell
+        PART = o; o += a16(size_t(2) * 2 * PX_NB * WAVE * 8);     // [parity][lane-set][block][lane]
+        REC = o;  o += a16(size_t(2) * 2 * PX_RF * WAVE * 4 + 16); // [parity][set][field][lane]; counts
+        CL = o;   o += a16(size_t(2) * WAVE);                     // compaction scratch
+        MLA = o;  o += a16(size_t(2) * NP * 8);                   // split part of qm, by span parity
+        Q5 = o;   o += a16(size_t(NP) * 8);
+        CT = o;   o += a16(size_t(CT_SIZE) * 4);
+        DT = o;   o += a16(size_t(DT_HP + N + 1) * 4);
+        PW = o;   o += a16(size_t(N + 9) * 4);                    // (expMLbase sigma)^t
+        BY = o;   o += a16(size_t(7) * NP);                       // S, up, dn, ptn, enc, flg, mat
+        BYTES = o;
+    }
+};
+
+struct PxL {
+    f2 *qb, *qm, *q1, *part, *mla, *q5;
+    float *rec, *ct, *dt, *pw;
+    int *rcnt;
+    uint8_t *cc, *cl, *S, *up, *dn, *ptn, *enc, *flg, *mat;
+    int N, NP;
+};
+
+__device__ __forceinline__ bool px_allowed(const PxL &L, int i, int j) {   // kernels.hip allowed()
+    const int fi = L.flg[i], fj = L.flg[j];
+    if ((fi | fj) & 1) return false;
+    if ((fi & 2) || (fj & 4)) return false;
+    const int pi = L.ptn[i], pj = L.ptn[j];
+    if (pi) return pi == j;
+    if (pj) return pj == i;
+    return L.enc[i] == L.enc[j];
+}
+
+// interior-loop shape kinds (dev_types.hpp TermKind; -1 = generic)
+__host__ __device__ constexpr int pkind(int n1, int n2) {
+    return (n1 == 0 && n2 == 0) ? TK_STK
+         : (n1 + n2 == 1) ? TK_B1
+         : (n1 == 0 || n2 == 0) ? TK_BUL
+         : (n1 == 1 && n2 == 1) ? TK_I11
+         : (n1 == 1 && n2 == 2) ? TK_I12
+         : (n1 == 2 && n2 == 1) ? TK_I21
+         : (n1 == 2 && n2 == 2) ? TK_I22
+         : ((n1 == 2 && n2 == 3) || (n1 == 3 && n2 == 2)) ? TK_M23
+         : (n1 == 1 || n2 == 1) ? TK_1N
+         : -1;
+}
+// constant factor of shape (u, n1) (adx_api.cpp addS / fgen); dz = 0 in every
+// lane but not provably uniform, so the factors of a B wave's sizes live in
+// VGPRs (as SGPRs they spill to lane slots, one v_readlane per use)
+__device__ __forceinline__ float shape_factor(const DevScaled *XS, int u, int n1, int dz) {
+    const int kd = pkind(n1, u - n1);
+    const float *p = kd < 0 ? XS->fgen + (u - 6) * FG_ROW + n1 - 2
+                   : kd == TK_STK ? XS->ctab + CT_FSM + 0
+                   : kd == TK_B1 ? XS->ctab + CT_FSM + 1
+                   : kd == TK_BUL ? XS->ctab + CT_FB + u
+                   : kd == TK_1N ? XS->ctab + CT_F1N + u - 1
+                   : kd == TK_I11 ? XS->ctab + CT_FSM + 2
+                   : kd == TK_I22 ? XS->ctab + CT_FSM + 4
+                   : kd == TK_M23 ? XS->ctab + CT_FSM + 5
+                   : XS->ctab + CT_FSM + 3;
+    return p[dz];
+}
+
+struct PxCell {              // per lane: the closing pair (i, i+s)
+    int i, ty8, A, B;
+    float tau, mo, m23;
+    float t11, t12, t21, t22;
+};
+
+// One shape (N1, U - N1): the inner cell (i+1+N1, j-1-U+N1) on diagonal s-2-U
+// at qb / cc row base + N1 (qb + o, cc + o: this lane's bases).
+template <int U, int N1, bool MK>
+__device__ __forceinline__ void pshape1(const PxL &L, const PxCell &c, const float *fv, const f2 *qb,
+                                        const uint8_t *cc, f2 &g, f2 &sp) {
+    constexpr int k = pkind(N1, U - N1);
+    constexpr int FI = N1 < U - N1 ? N1 : U - N1;
+    f2 v = qb[N1];
+    if constexpr (MK) v = (N1 <= c.A && U - N1 <= c.B) ? v : f2{0.f, 0.f};
+    if constexpr (k < 0) {
+        g.x = fmaf(v.x, fv[FI], g.x);   // scalar FMAs: a packed one wants the factor duplicated in a register pair
+        g.y = fmaf(v.y, fv[FI], g.y);
+    } else {
+        const float *ct = L.ct;
+        const int ci = cc[N1];
+        float f;
+        if constexpr (k == TK_STK || k == TK_B1) {
+            f = ct[CT_INVMM + ci] * ct[CT_STK + c.ty8 + ((ci * 41) >> 10)] * fv[FI];
+        } else if constexpr (k == TK_BUL) {
+            f = ct[CT_BUL + ci] * (c.tau * fv[FI]);
+        } else if constexpr (k == TK_1N) {
+            f = ct[CT_ONEN + ci] * (c.mo * fv[FI]);
+        } else if constexpr (k == TK_M23) {
+            f = ct[CT_INVMM + ci] * ct[CT_M23O + ci] * (c.m23 * fv[FI]);
+        } else {
+            const float tv = k == TK_I11 ? c.t11 : k == TK_I12 ? c.t12 : k == TK_I21 ? c.t21 : c.t22;
+            f = ct[CT_INVMM + ci] * (tv * fv[FI]);
+        }
+        sp = fma2(v, sp2(f), sp);
+    }
+}
+template <int U, bool MK, int... N1s>
+__device__ __forceinline__ void pshape_seq(std::integer_sequence<int, N1s...>, const PxL &L, const PxCell &c,
+                                           const float *fv, const f2 *qb, const uint8_t *cc, f2 &g, f2 &sp) {
+    (pshape1<U, N1s, MK>(L, c, fv, qb, cc, g, sp), ...);
+}
+// every shape factor is symmetric in (n1, n2) (adx_api.cpp build_scaled): a
+// size keeps U/2 + 1 of them, shape n1 reads fv[min(n1, U - n1)]
+template <int U>
+struct PxSize {
+    float fv[U < 0 ? 1 : U / 2 + 1];
+    __device__ __forceinline__ void load(const DevScaled *XS, int dz) {
+        if constexpr (U >= 0)
+#pragma unroll
+            for (int n1 = 0; n1 <= U / 2; n1++) fv[n1] = shape_factor(XS, U, n1, dz);
+    }
+    template <bool MK>
+    __device__ __forceinline__ void run(const PxL &L, const PxCell &c, int s, int umax, f2 &g, f2 &sp) const {
+        if constexpr (U >= 0) {
+            if (U <= umax) {
+                const int o = off(s - 2 - U, L.N) + c.i;   // inner cell (i+1+n1, ...) at o + n1
+                pshape_seq<U, MK>(std::make_integer_sequence<int, U + 1>{}, L, c, fv, L.qb + o, L.cc + o, g, sp);
+            }
+        }
+    }
+};
+
+#ifdef ADX_STAMP
+__device__ unsigned long long g_stamps_p[16][8];
+#define PSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#define PX_STP_PARAMS , unsigned long long *st_acc, unsigned long long &st_last
+#define PX_STP_ARGS , st_acc, st_last
+#else
+#define PSTAMP(k) do { } while (0)
+#define PX_STP_PARAMS
+#define PX_STP_ARGS
+#endif
+
+// B: interior-loop sums of every diagonal for one block of loop sizes, the
+// block's shape factors in registers for the whole sweep; writes the partial
+// of each compacted pairable cell to its natural slot.
+template <int U0, int U1, int U2, int U3>
+__device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int N, int lane, int wid,
+                                         bool constrained, int s_end PX_STP_PARAMS) {
+    constexpr bool TB = (U0 >= 2 && U0 <= 4) || (U1 >= 2 && U1 <= 4) || (U2 >= 2 && U2 <= 4) || (U3 >= 2 && U3 <= 4);
+    PxSize<U0> s0;
+    PxSize<U1> s1;
+    PxSize<U2> s2;
+    PxSize<U3> s3;
+    // uniform factors: SGPRs (a VALU FMA reads one SGPR operand for free)
+    s0.load(XS, 0);
+    s1.load(XS, 0);
+    s2.load(XS, 0);
+    s3.load(XS, 0);
+    for (int s = 4; s <= s_end; s++) {
+        const int par = s & 1;
+        const int umax = min(30, s - 6);   // no interior loop fits a span below 6
+        const int ncls = (s <= N - 1 && umax >= 0) ? (uni(L.rcnt[par]) + WAVE - 1) / WAVE : 0;
+        for (int ls = 0; ls < ncls; ls++) {
+            const float *r = L.rec + ((par * 2 + ls) * PX_RF) * WAVE + lane;
+            const int fl = __float_as_int(r[WAVE]);
+            PxCell c;
+            c.i = __float_as_int(r[0]);
+            c.ty8 = (fl & 7) * 8;
+            c.A = (fl >> 8) & 255;
+            c.B = (fl >> 16) & 255;
+            const float mmo = r[2 * WAVE];
+            c.tau = r[3 * WAVE];
+            c.mo = r[4 * WAVE];
+            c.m23 = r[5 * WAVE];
+            c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
+            if constexpr (TB) {
+                c.t11 = r[6 * WAVE];
+                c.t12 = r[7 * WAVE];
+                c.t21 = r[8 * WAVE];
+                c.t22 = r[9 * WAVE];
+            }
+            f2 g = {0.f, 0.f}, sp = {0.f, 0.f};
+            PSTAMP(2);
+            // shapes past a cell's allowed unpaired runs (constraints) are masked
+            const bool mk = constrained && __ballot((fl >> 24) & 1) != 0;
+            if (mk) {
+                s0.template run<true>(L, c, s, umax, g, sp);
+                s1.template run<true>(L, c, s, umax, g, sp);
+                s2.template run<true>(L, c, s, umax, g, sp);
+                s3.template run<true>(L, c, s, umax, g, sp);
+            } else {
+                s0.template run<false>(L, c, s, umax, g, sp);
+                s1.template run<false>(L, c, s, umax, g, sp);
+                s2.template run<false>(L, c, s, umax, g, sp);
+                s3.template run<false>(L, c, s, umax, g, sp);
+            }
+            PSTAMP(3);
+            if ((fl >> 25) & 1)   // a real cell (not an idle lane)
+                L.part[((par * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] =
+                    fma2(g, sp2(mmo), sp);
+        }
+        PSTAMP(5);
+        lds_barrier();
+        PSTAMP(6);
+    }
+}
+
+// One workgroup per (walker, group).  gout: [W][n_variants] ensemble energies
+// (kcal/mol, as score_sequence writes dG), the scores follow in combine_kernel.
+__global__ void __launch_bounds__(PX_NT, 1)
+pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
+                float *gout) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int w = blockIdx.x / ka.n_groups2, grp = blockIdx.x % ka.n_groups2;
+    if (w >= W) return;
+    if (mask && mask[w] != 1) return;
+    const int vs0 = ka.groups2[2 * grp], vs1 = ka.groups2[2 * grp + 1];
+    const DevVariant V = ka.variants[vs0];
+    const bool hol0 = ka.variants[vs0].motif != 0, hol1 = ka.variants[vs1].motif != 0;
+    const int N = uni(V.N);
+    const PxLay Y(N);
+    PxL L;
+    L.qb = reinterpret_cast<f2 *>(smem + Y.QB);
+    L.qm = reinterpret_cast<f2 *>(smem + Y.QM);
+    L.q1 = reinterpret_cast<f2 *>(smem + Y.Q1);
+    L.cc = reinterpret_cast<uint8_t *>(smem + Y.CC);
+    L.part = reinterpret_cast<f2 *>(smem + Y.PART);
+    L.rec = reinterpret_cast<float *>(smem + Y.REC);
+    L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(2) * 2 * PX_RF * WAVE * 4);
+    L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);
+    L.mla = reinterpret_cast<f2 *>(smem + Y.MLA);
+    L.q5 = reinterpret_cast<f2 *>(smem + Y.Q5);
+    L.ct = reinterpret_cast<float *>(smem + Y.CT);
+    L.dt = reinterpret_cast<float *>(smem + Y.DT);
+    L.pw = reinterpret_cast<float *>(smem + Y.PW);
+    uint8_t *by = reinterpret_cast<uint8_t *>(smem + Y.BY);
+    L.S = by;
+    L.up = by + Y.NP;
+    L.dn = by + 2 * Y.NP;
+    L.ptn = by + 3 * Y.NP;
+    L.enc = by + 4 * Y.NP;
+    L.flg = by + 5 * Y.NP;
+    L.mat = by + 6 * Y.NP;
+    L.N = N;
+    L.NP = Y.NP;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
+    const int C = Y.C, NP = Y.NP;
+    const DevTables &T = *ka.T;
+#ifdef ADX_STAMP
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
+
+    // ---- incremental fold state (kernels.hip score_sequence / Inc): this group's
+    // tables of the current sequence (src) and the proposal's (dst)
+    const size_t Cs = size_t(ka.cells), B1 = 3 * Cs + size_t(ka.Nmax) + 2;
+    const float *src = nullptr;
+    float *dst = nullptr;
+    int m_lo = 0, m_hi = 0;
+    if (ka.tab) {
+        const int cur = ka.cur_slot[w];
+        float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
+        dst = base + size_t(1 - cur) * ka.tab_slot + size_t(grp) * 2 * B1;
+        if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+            src = base + size_t(cur) * ka.tab_slot + size_t(grp) * 2 * B1;
+            m_lo = ka.chg[2 * w] + 1 + V.before_len;
+            m_hi = ka.chg[2 * w + 1] + 1 + V.before_len;
+        }
+    }
+    const bool incr = src != nullptr;
+    m_lo = uni(m_lo);
+    m_hi = uni(m_hi);
+    auto clo = [&](int D) { return incr ? max(1, m_lo - 1 - D) : 1; };
+    auto chi = [&](int D) { return incr ? min(N - D, m_hi + 1) : N - D; };
+    auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
+    auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
+
+    // ---- sequence, constraint arrays, tables (kernels.hip pf_group setup)
+    const uint8_t *cons = ka.cons + V.cons_off;
+    {
+        const uint8_t *bef = nullptr, *aft = nullptr;
+        int blen = 0;
+        if (V.ctx >= 0) {
+            bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
+            blen = ka.ctx_off[4 * V.ctx + 1];
+            aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
+        }
+        const uint8_t *raw = seqs + size_t(w) * ka.Nraw;
+        for (int k = tid; k < NP; k += PX_NT) {
+            uint8_t s = 0;
+            if (k >= 1 && k <= N) {
+                const int pp = k - 1;
+                if (pp < blen) s = bef[pp];
+                else if (pp < blen + ka.Nraw) s = raw[pp - blen];
+                else s = aft[pp - blen - ka.Nraw];
+            }
+            L.S[k] = s;
+            L.up[k] = cons[k];
+            L.dn[k] = cons[NP + k];
+            L.ptn[k] = cons[2 * NP + k];
+            L.enc[k] = cons[3 * NP + k];
+            L.flg[k] = cons[4 * NP + k];
+            L.mat[k] = 0;
+        }
+    }
+    bool cst = false;
+    for (int k = 1 + tid; k <= N; k += PX_NT) cst |= (L.flg[k] | L.ptn[k]) != 0;
+    for (int k = tid; k < CT_SIZE; k += PX_NT) L.ct[k] = XS->ctab[k];
+    for (int k = tid; k < 200; k += PX_NT) {
+        L.dt[DT_MMH + k] = (&T.mmH[0][0][0])[k];
+        L.dt[DT_MMI + k] = (&T.mmI[0][0][0])[k];
+        L.dt[DT_MLS + k] = (&T.mlstem[0][0][0])[k];
+    }
+    for (int k = tid; k < 288; k += PX_NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
+    for (int k = tid; k < 8; k += PX_NT) L.dt[DT_TAU + k] = T.termAU[k];
+    for (int k = tid; k <= N; k += PX_NT) L.dt[DT_HP + k] = XS->hp[k];
+    for (int k = tid; k < N + 9; k += PX_NT) L.pw[k] = XS->pwml[k];
+    for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
+    for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
+    const bool constrained = __syncthreads_or(cst);
+    if (tid == 0) {   // ViennaRNA's S1 wrap-around
+        L.S[0] = L.S[N];
+        L.S[N + 1] = L.S[1];
+    }
+    const int mL = XS->motif_len;
+    const bool any_motif = (hol0 || hol1) && mL > 0;
+    __syncthreads();
+    if (any_motif) {
+        for (int o = tid + 1; o + mL - 1 <= N; o += PX_NT) {
+            bool ok = true;
+            for (int k = 0; k < mL && ok; k++)
+                if (L.S[o + k] != XS->motif_code[k]) ok = false;
+            for (int k = 0; k < mL && ok; k++) {
+                const int pk = XS->motif_pt[k];
+                if (pk < 0) ok = L.up[o + k] >= 1;
+                else if (pk > k) ok = px_allowed(L, o + k, o + pk);
+            }
+            L.mat[o] = ok ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    const uint8_t *S = L.S;
+    const float *ct = L.ct;
+    const float sig1 = XS->sig[1], mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing;
+    const float eTAU = XS->ctab[CT_FSM + 6];
+    const float mext = XS->motif_extra;
+    const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
+
+    // every cell, one flat pass: inner code; changed cells: the hairpin (+ motif)
+    // initial value (pairable) or the mark, the multiloop stem in qm1 (F reads
+    // both before overwriting); unchanged cells and q5 from the current tables
+    for (int k = tid; k < C; k += PX_NT) {
+        int D = 4;
+        {   // diagonal of the diagonal-major index k
+            const float b = float(2 * N - 7);
+            D = 4 + int((b - sqrtf(fmaxf(b * b - 8.f * float(k), 0.f))) * 0.5f);
+            D = D < 4 ? 4 : D;
+            while (D < N - 1 && off(D + 1, N) <= k) D++;
+            while (D > 4 && off(D, N) > k) D--;
+        }
+        const int i = k - off(D, N) + 1, j = i + D;
+        const int type = ptype(S[i], S[j]);
+        L.cc[k] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
+        const int rq = rowb(i, N) + D - 4, r1 = colb(j) + i - 1;
+        if (incr && (i < clo(D) || i > chi(D))) {
+            L.qb[k] = f2{src[k], src[B1 + k]};
+            L.q1[r1] = f2{src[2 * Cs + r1], src[B1 + 2 * Cs + r1]};
+        } else {
+            const bool pr = type != 0 && px_allowed(L, i, j);
+            f2 init = f2{-0.f, -0.f};
+            float m1 = 0.f;
+            if (pr) {
+                const int u = D - 1;
+                float h = 0.f;
+                if (L.up[i + 1] >= u) {
+                    bool special = false;
+                    if (u == 3 || u == 4 || u == 6) {
+                        const uint32_t key = hp_key(S, i, u + 2);
+                        for (int q = 0; q < nsp; q++)
+                            if (XS->sp_key[q] == key) { h = XS->sp_val[q]; special = true; break; }
+                    }
+                    if (!special)
+                        h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type] : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
+                }
+                const bool mx = D == mL - 1 && mL > 0 && L.mat[i];
+                init = f2{(mx && hol0) ? h + mext : h, (mx && hol1) ? h + mext : h};
+                m1 = L.dt[DT_MLS + type * 25 + S[i - 1] * 5 + S[j + 1]];
+            }
+            L.qb[k] = init;
+            L.q1[r1] = f2{m1, m1};
+        }
+        // qm: unchanged items from src (changed ones are written by M)
+        if (incr && D <= N - 3 && (i < qlo(D) || i > qhi(D))) L.qm[rq] = f2{src[Cs + rq], src[B1 + Cs + rq]};
+        else L.qm[rq] = f2{0.f, 0.f};
+    }
+    for (int k = tid; k <= N; k += PX_NT) {
+        if (incr && k <= m_lo - 2) {
+            L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
+        } else if (k <= 3) {   // q5[0..3] (pf_group: unpaired prefix)
+            float q = 1.f;
+            bool ok = true;
+            for (int t = 1; t <= k; t++) {
+                ok = ok && L.up[t] >= 1;
+                q *= sig1;
+            }
+            L.q5[k] = ok ? f2{q, q} : f2{0.f, 0.f};
+        }
+    }
+    __syncthreads();
+    PSTAMP(0);
+
+    // ---- records (wave 13): compaction of the changed pairable cells of
+    // diagonal D and their setup values (outer factors of the closing pair, the
+    // 1x1..2x2 table factors, the unpaired runs), written at step D - 1
+    auto rec_make = [&](int D) {
+        if (D < 6 || D > N - 1) {
+            if (lane == 0) L.rcnt[D & 1] = 0;
+            return;
+        }
+        const int lo = clo(D), hi = chi(D);
+        int base = 0;
+        for (int i0 = lo; i0 <= hi; i0 += WAVE) {
+            const int i = i0 + lane;
+            const bool pr = i <= hi && !is_mark2(L.qb[off(D, N) + i - 1]);
+            const uint64_t m = __ballot(pr);
+            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            if (pr) L.cl[slot] = uint8_t(i);
+            base += __popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int umax = min(30, D - 6);
+        for (int k = 0; k * WAVE < base; k++) {
+            const int idx = k * WAVE + lane;
+            const bool v = idx < base;
+            const int i = v ? L.cl[idx] : int(L.cl[0]), j = i + D;
+            const int ty = ptype(S[i], S[j]);
+            const int si1 = S[i + 1], sj1 = S[j - 1];
+            const int oc = ty * 25 + si1 * 5 + sj1;
+            const int A = L.up[i + 1], Bq = L.dn[j - 1];
+            float t11 = 0.f, t12 = 0.f, t21 = 0.f, t22 = 0.f;
+            // kernels.hip load_chunk: lane-4c+g table factors, here per cell
+            auto t2of = [&](int n1, int n2) { return (L.cc[off(D - 2 - n1 - n2, N) + i + n1] * 41) >> 10; };
+            if (umax >= 2) t11 = T.int11[ty][t2of(1, 1)][si1][sj1];
+            if (umax >= 3) {
+                t12 = T.int21[ty][t2of(1, 2)][si1][S[j - 2]][sj1];
+                t21 = T.int21[t2of(2, 1)][ty][sj1][si1][S[i + 2]];
+            }
+            if (umax >= 4) t22 = T.int22[ty][t2of(2, 2)][si1][S[i + 2]][S[j - 2]][sj1];
+            const float mmo = L.dt[DT_MMI + oc];
+            float *r = L.rec + (((D & 1) * 2 + k) * PX_RF) * WAVE + lane;
+            const bool mkc = A < umax || Bq < umax;
+            r[0] = __int_as_float(i);
+            r[WAVE] = __int_as_float(ty | (A << 8) | (Bq << 16) | (mkc ? (1 << 24) : 0) | (v ? (1 << 25) : 0));
+            r[2 * WAVE] = mmo;
+            r[3 * WAVE] = ty > 2 ? eTAU : 1.f;
+            r[4 * WAVE] = ct[CT_ONEN + oc] * mmo;
+            r[5 * WAVE] = ct[CT_M23O + oc];
+            r[6 * WAVE] = t11;
+            r[7 * WAVE] = t12;
+            r[8 * WAVE] = t21;
+            r[9 * WAVE] = t22;
+        }
+        if (lane == 0) L.rcnt[D & 1] = base;
+    };
+    if (wid == PX_NW - 1) rec_make(4);   // the sweep's first B diagonal (no loop fits: count 0)
+    __syncthreads();
+
+    const int s_end = N + 1;
+    if (wid < PX_NB) {
+        switch (wid) {
+            // sizes U, U' with U + U' = 29 cost 31 shape reads together: two such
+            // units (or 30 alone) per wave
+            case 0: pb_sweep<30, 29, 0, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<28, 1, 27, 2>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 2: pb_sweep<26, 3, 25, 4>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<24, 5, 23, 6>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<22, 7, 21, 8>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<20, 9, 19, 10>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<18, 11, 17, 12>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            default: pb_sweep<16, 13, 15, 14>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+        }
+    } else {
+        for (int s = 4; s <= s_end; s++) {
+            if (wid < PX_NB + PX_NMW) {
+                // ---------------- M: qm items of span sq = s - 2, K lanes per item
+                // (power of two, items x K <= the M waves' lanes), split points in
+                // contiguous runs per lane, summed over the K lanes:
+                //   qm(i, jb)  = sum_t [t <= up_i] pw(t) qm1(i+t, jb) + sum_{t >= 5} qm(i, i+t-1) qm1(i+t, jb)
+                //   mla(i, sq) = the split part
+                const int sq = s - 2;
+                if (sq >= 4 && sq <= N - 3) {
+                    const int lo = qlo(sq), n = qhi(sq) - lo + 1;
+                    // K from the full fold's item count: a refold sums every item in
+                    // the same order as a fold from scratch (bit-identical tables)
+                    int K = 16;
+                    while (K > 1 && (N - sq) * K > PX_NMW * WAVE) K >>= 1;
+                    const int ipw = WAVE / K;                 // items per wave
+                    const int mw = wid - PX_NB;
+                    if (mw * ipw < n) {
+                        const int item = mw * ipw + lane / K, k = lane & (K - 1);
+                        const bool valid = item < n;
+                        const int i = lo + (valid ? item : n - 1);
+                        const int jb = i + sq, T = sq - 4;
+                        const int tch = (T + K) / K;          // split points per lane
+                        const int t0 = k * tch, t1 = min(T, t0 + tch - 1);
+                        const int upi = constrained ? L.up[i] : 255;
+                        const f2 *pq = L.q1 + colb(jb) + i - 1;   // qm1(i+t, jb) at +t
+                        const f2 *pr = L.qm + rowb(i, N) - 5;      // qm(i, i+t-1) at +t (t >= 5)
+                        f2 A = {0.f, 0.f}, A1 = {0.f, 0.f}, Pp = {0.f, 0.f};
+                        for (int t = t0; t <= t1; t += 8) {
+                            f2 qv[8], rv[8];
+                            float wv[8];
+#pragma unroll
+                            for (int kk = 0; kk < 8; kk++) {
+                                qv[kk] = pq[t + kk];
+                                rv[kk] = pr[(t + kk >= 5) ? t + kk : 5];
+                                wv[kk] = L.pw[t + kk];
+                            }
+#pragma unroll
+                            for (int kk = 0; kk < 8; kk++) {
+                                const int tt = t + kk;
+                                const f2 q = tt <= t1 ? qv[kk] : f2{0.f, 0.f};
+                                Pp = fma2(sp2(tt <= upi ? wv[kk] : 0.f), q, Pp);
+                                if (kk & 1) A1 = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A1);
+                                else A = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A);
+                            }
+                        }
+                        A += A1;
+                        for (int o = 1; o < K; o <<= 1) {
+                            A.x += __shfl_xor(A.x, o, WAVE);
+                            A.y += __shfl_xor(A.y, o, WAVE);
+                            Pp.x += __shfl_xor(Pp.x, o, WAVE);
+                            Pp.y += __shfl_xor(Pp.y, o, WAVE);
+                        }
+                        if (valid && k == 0) {
+                            L.qm[rowb(i, N) + sq - 4] = A + Pp;
+                            L.mla[(sq & 1) * NP + i] = A;
+                        }
+                    }
+                }
+            } else if (wid == PX_NB + PX_NMW) {
+                // ---------------- F: the changed cells of diagonal e = s - 1
+                const int e = s - 1;
+                if (e >= 4 && e <= N - 1) {
+                    const int lo = clo(e), hi = chi(e);
+                    for (int i0 = lo; i0 <= hi; i0 += WAVE) {
+                        const int i = i0 + lane;
+                        if (i > hi) break;
+                        const int j = i + e;
+                        const int ce = off(e, N) + i - 1, c1 = colb(j) + i - 1;
+                        const f2 init = L.qb[ce];
+                        const f2 stem = L.q1[c1];
+                        const bool upj = e >= 5 && L.up[j] >= 1;
+                        const f2 prev = upj ? L.q1[colb(j - 1) + i - 1] : f2{0.f, 0.f};
+                        if (!is_mark2(init)) {
+                            const int ty = ptype(S[i], S[j]);
+                            const float mlcl = mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
+                            f2 a_int = {0.f, 0.f};
+                            if (e >= 6) {
+                                const f2 *pp = L.part + ((e & 1) * 2 + ((i - 1) >> 6)) * PX_NB * WAVE + ((i - 1) & (WAVE - 1));
+#pragma unroll
+                                for (int b = 0; b < PX_NB; b++) a_int += pp[b * WAVE];
+                            }
+                            const f2 ml = e - 2 >= 4 ? L.mla[((e - 2) & 1) * NP + i + 1] : f2{0.f, 0.f};
+                            const f2 qb = a_int + init + ml * sp2(mlcl);
+                            const float mmc = L.dt[DT_MMI + L.cc[ce]];
+                            L.qb[ce] = qb * sp2(mmc) + f2{0.f, 0.f};   // never the mark (-0)
+                            L.q1[c1] = fma2(qb, stem, prev * sp2(mlbase_sig));
+                        } else {
+                            L.q1[c1] = prev * sp2(mlbase_sig);
+                        }
+                    }
+                }
+            } else if (wid == PX_NB + PX_NMW + 1) {
+                // ---------------- Q: q5[j], j = s - 1 (column j is final)
+                const int j = s - 1;
+                if (j >= 4 && j <= N && (!incr || j >= m_lo - 1)) {
+                    const int sjp = (j < N) ? S[j + 1] : 5;
+                    const int sj = S[j];
+                    f2 acc = {0.f, 0.f};
+                    for (int k0 = 1; k0 <= j - 4; k0 += WAVE) {
+                        const int kk = k0 + lane;
+                        const bool ok = kk <= j - 4;
+                        const int k = ok ? kk : 1;
+                        const int ix = off(j - k, N) + k - 1;
+                        const int ty = ptype(S[k], sj);
+                        const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? S[k - 1] : 5) * 6 + sjp];
+                        const float f = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
+                        acc = fma2(L.q5[k - 1] * L.qb[ix], sp2(f), acc);
+                    }
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        acc.x += __shfl_xor(acc.x, o, WAVE);
+                        acc.y += __shfl_xor(acc.y, o, WAVE);
+                    }
+                    if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sp2(sig1) : f2{0.f, 0.f}) + acc;
+                }
+            } else if (wid == PX_NW - 1) {
+                // ---------------- R: records of diagonal s + 1 (next step's B)
+                rec_make(s + 1);
+            }
+            PSTAMP(4);
+            lds_barrier();
+            PSTAMP(6);
+        }
+    }
+#ifdef ADX_STAMP
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
+#endif
+    __syncthreads();
+    // ---- the proposal's tables (the next step's unchanged cells) and the energies
+    if (dst) {
+        for (int k = tid; k < C; k += PX_NT) {
+            const f2 a = L.qb[k], b = L.qm[k], c = L.q1[k];
+            dst[k] = a.x;
+            dst[B1 + k] = a.y;
+            dst[Cs + k] = b.x;
+            dst[B1 + Cs + k] = b.y;
+            dst[2 * Cs + k] = c.x;
+            dst[B1 + 2 * Cs + k] = c.y;
+        }
+        for (int k = tid; k <= N; k += PX_NT) {
+            dst[3 * Cs + k] = L.q5[k].x;
+            dst[B1 + 3 * Cs + k] = L.q5[k].y;
+        }
+    }
+    if (tid == 0) {   // ensemble energy -kT (ln Z_scaled - N ln sigma), as vrna_pf (float)
+        const f2 z = L.q5[N];
+        gout[size_t(w) * ka.n_variants + vs0] = float(-XS->kT * (log(double(z.x)) - N * XS->log_sigma));
+        gout[size_t(w) * ka.n_variants + vs1] = float(-XS->kT * (log(double(z.y)) - N * XS->log_sigma));
+    }
+}
+
+}  // namespace
+
+// LDS bytes of the lanes = cells PF kernel for this workload (0: not covered)
+size_t pf_cells_lds(const KArgs &ka) {
+    if (ka.mode != 0 || ka.Nmax > PX_NMAX || ka.Nmax < 8) return 0;
+    const size_t b = PxLay(ka.Nmax).BYTES;
+    return b + 256 <= 160 * 1024 ? b : 0;
+}
+
+hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
+                           hipStream_t stream) {
+    const size_t lds = pf_cells_lds(ka);
+    if (lds == 0) return hipErrorInvalidValue;
+    static size_t configured = 0;
+    if (lds > configured) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(pf_cells_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        configured = lds;
+    }
+    hipLaunchKernelGGL(pf_cells_kernel, dim3(W * ka.n_groups2), dim3(PX_NT), lds, stream, ka, ka.X, seqs, W, mask,
+                       gout);
+    return hipGetLastError();
+}
+
+}  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps_pf(unsigned long long *out, int reset) {  // [16][8]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_p), sizeof(adx::g_stamps_p)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_p), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif

@@ -223,3 +223,39 @@ def test_mc_pf_incremental_consistency(native, oracle):
     sc, _, _ = eng.score_batch(final)
     for w in range(W):
         assert scores[w] == sc[w] or abs(scores[w] - sc[w]) <= 1e-6 * max(1.0, abs(sc[w])), (w, scores[w], sc[w])
+
+
+@pytest.mark.parametrize("kernel", ["rows", "cells"])
+def test_pf_kernels_score_and_trajectory(native, oracle, monkeypatch, kernel):
+    """The general PF kernel (score_kernel<SumProd>, lanes = terms: lengths the
+    cells kernel does not cover) and the default pf_cells_kernel (lanes = cells),
+    selected per launch by ADX_PF_KERNEL: ensemble energies within DG_TOL of the
+    oracle over two macrostates and three contexts, and an incremental MC
+    trajectory identical to the oracle's."""
+    monkeypatch.setenv("ADX_PF_KERNEL", kernel)
+    tmpl, active = workloads.synthetic(90)
+    other = "." * 12 + "(" + "." * 30 + ")" + "." * (90 - 44)
+    terms = [("apo", 0, False, 1.0), ("holo", 0, True, 0.5), ("apo", 1, True, 2.0)]
+    ctx = [("GGAC", "UUA"), ("", "CCCA"), ("AUAUA", "")]
+    eng = _engine(native, tmpl, [active, other], terms, contexts=ctx)
+    seqs = workloads.walker_sequences(tmpl, [active, other], 8)
+    sc, tv, dg = eng.score_batch(seqs)
+    sf = _oracle_sf(oracle, terms, contexts=ctx)
+    for w in range(8):
+        ref, tref = sf.score(seqs[w], [active, other])
+        assert abs(sc[w] - ref) <= 5e-3, (kernel, w, sc[w], ref)
+        assert np.allclose(tv[w], tref, atol=2e-3), (kernel, w)
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seqs = workloads.walker_sequences(tmpl, [active], 16)
+    _, _, dg = eng.score_batch(seqs)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(0, 16, 3):
+            ref = oracle.pf_energy(seqs[w], active if mac >= 0 else None, motif if cond == 1 else None)
+            assert abs(dg[w, v] - np.float32(ref)) <= DG_TOL, (kernel, v, w, dg[w, v], ref)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    _replay(oracle, native, eng, tmpl, [active], terms, therm_o, [21, 22, 23, 24], seqs[:4], 30)
