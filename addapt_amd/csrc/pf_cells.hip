@@ -46,6 +46,27 @@ constexpr int PX_SLACK = 16;
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 sp2(float x) { return f2{x, x}; }
 __device__ __forceinline__ bool is_mark2(f2 v) { return __float_as_uint(v.x) == 0x80000000u; }
+// sum of v over the wave, both components (permlane32 swap folds x into lanes
+// 0-31 and y into 32-63, one DPP chain finishes both; VALU only)
+__device__ __forceinline__ f2 wave_sum_f2(f2 v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v.x), __float_as_uint(v.y), false, false);
+    // lanes 0-31: x(l) + x(l+32); lanes 32-63: y(l-32) + y(l)
+    float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    t += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0xb1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+    t += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x4e, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+    t += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x114, 0xf, 0xf, false));  // row_shr:4
+    t += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x118, 0xf, 0xf, false));  // row_shr:8
+    t += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(t), 0x142, 0xa, 0xf, false));  // row_bcast:15
+    return f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 31)),
+              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 63))};
+}
+// v + (v of the lane DPP control CTRL selects; 0 where it selects none)
+template <int CTRL>
+__device__ __forceinline__ f2 dpp_add2(f2 v) {
+    const float x = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.x), CTRL, 0xf, 0xf, false));
+    const float y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.y), CTRL, 0xf, 0xf, false));
+    return v + f2{x, y};
+}
 
 struct PxLay {
     int C, NP;
@@ -61,7 +82,7 @@ struct PxLay {
         CC = o;   o += a16(size_t(C) + PX_SLACK);                 // inner-pair code per cell
         PART = o; o += a16(size_t(2) * 2 * PX_NB * WAVE * 8);     // [parity][lane-set][block][lane]
         REC = o;  o += a16(size_t(2) * 2 * PX_RF * WAVE * 4 + 16); // [parity][set][field][lane]; counts
-        CL = o;   o += a16(size_t(2) * WAVE);                     // compaction scratch
+        CL = o;   o += a16(size_t(C) + size_t(NP));               // rank lists of the changed pairable cells + counts
         MLA = o;  o += a16(size_t(2) * NP * 8);                   // split part of qm, by span parity
         Q5 = o;   o += a16(size_t(NP) * 8);
         CT = o;   o += a16(size_t(CT_SIZE) * 4);
@@ -76,7 +97,7 @@ struct PxL {
     f2 *qb, *qm, *q1, *part, *mla, *q5;
     float *rec, *ct, *dt, *pw;
     int *rcnt;
-    uint8_t *cc, *cl, *S, *up, *dn, *ptn, *enc, *flg, *mat;
+    uint8_t *cc, *cl, *cn, *S, *up, *dn, *ptn, *enc, *flg, *mat;
     int N, NP;
 };
 
@@ -130,11 +151,13 @@ struct PxCell {              // per lane: the closing pair (i, i+s)
 // at qb / cc row base + N1 (qb + o, cc + o: this lane's bases).
 template <int U, int N1, bool MK>
 __device__ __forceinline__ void pshape1(const PxL &L, const PxCell &c, const float *fv, const f2 *qb,
-                                        const uint8_t *cc, f2 &g, f2 &sp) {
+                                        const uint8_t *cc, uint32_t bits, f2 &g, f2 &sp) {
     constexpr int k = pkind(N1, U - N1);
     constexpr int FI = N1 < U - N1 ? N1 : U - N1;
     f2 v = qb[N1];
-    if constexpr (MK) v = (N1 <= c.A && U - N1 <= c.B) ? v : f2{0.f, 0.f};
+    // constrained cell: shapes past its unpaired runs count 0 (bit N1 of the size's
+    // allowed-n1 mask as a factor: a compare-select becomes a branch around the load)
+    if constexpr (MK) v *= sp2(float((bits >> N1) & 1u));
     if constexpr (k < 0) {
         g.x = fmaf(v.x, fv[FI], g.x);   // scalar FMAs: a packed one wants the factor duplicated in a register pair
         g.y = fmaf(v.y, fv[FI], g.y);
@@ -159,8 +182,9 @@ __device__ __forceinline__ void pshape1(const PxL &L, const PxCell &c, const flo
 }
 template <int U, bool MK, int... N1s>
 __device__ __forceinline__ void pshape_seq(std::integer_sequence<int, N1s...>, const PxL &L, const PxCell &c,
-                                           const float *fv, const f2 *qb, const uint8_t *cc, f2 &g, f2 &sp) {
-    (pshape1<U, N1s, MK>(L, c, fv, qb, cc, g, sp), ...);
+                                           const float *fv, const f2 *qb, const uint8_t *cc, uint32_t bits, f2 &g,
+                                           f2 &sp) {
+    (pshape1<U, N1s, MK>(L, c, fv, qb, cc, bits, g, sp), ...);
 }
 // every shape factor is symmetric in (n1, n2) (adx_api.cpp build_scaled): a
 // size keeps U/2 + 1 of them, shape n1 reads fv[min(n1, U - n1)]
@@ -177,7 +201,13 @@ struct PxSize {
         if constexpr (U >= 0) {
             if (U <= umax) {
                 const int o = off(s - 2 - U, L.N) + c.i;   // inner cell (i+1+n1, ...) at o + n1
-                pshape_seq<U, MK>(std::make_integer_sequence<int, U + 1>{}, L, c, fv, L.qb + o, L.cc + o, g, sp);
+                uint32_t bits = 0;
+                if constexpr (MK) {   // n1 <= A and U - n1 <= B
+                    const int lo = max(0, U - c.B), hi = min(U, c.A);
+                    bits = hi < lo ? 0u : ((2u << hi) - 1u) & ~((1u << lo) - 1u);
+                }
+                pshape_seq<U, MK>(std::make_integer_sequence<int, U + 1>{}, L, c, fv, L.qb + o, L.cc + o, bits, g,
+                                  sp);
             }
         }
     }
@@ -281,7 +311,8 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     L.part = reinterpret_cast<f2 *>(smem + Y.PART);
     L.rec = reinterpret_cast<float *>(smem + Y.REC);
     L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(2) * 2 * PX_RF * WAVE * 4);
-    L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);
+    L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);       // cl[off(D) + rank] = i
+    L.cn = L.cl + Y.C;                                      // cn[D] = count
     L.mla = reinterpret_cast<f2 *>(smem + Y.MLA);
     L.q5 = reinterpret_cast<f2 *>(smem + Y.Q5);
     L.ct = reinterpret_cast<float *>(smem + Y.CT);
@@ -371,6 +402,28 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     for (int k = tid; k < N + 9; k += PX_NT) L.pw[k] = XS->pwml[k];
     for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
     for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
+    if (incr) {
+        // refold: every table from the current slot (the changed cells are
+        // recomputed over it), two cells per lane and load, both folds interleaved
+        // (HBM side dword-aligned only when cells or B1 are odd: fine for global loads)
+        float4 *qd = reinterpret_cast<float4 *>(L.qb);   // qb, qm, q1 contiguous at a16(C + slack) strides
+        const int half = C >> 1;
+        const size_t ls4 = (Y.QM - Y.QB) >> 4;
+#pragma unroll 4
+        for (int k = tid; k < 3 * half; k += PX_NT) {
+            const int a = k / half, c = k - a * half;
+            const float *sa = src + a * Cs + 2 * c;
+            const float2 x = *reinterpret_cast<const float2 *>(sa), y = *reinterpret_cast<const float2 *>(sa + B1);
+            qd[a * ls4 + c] = float4{x.x, y.x, x.y, y.y};
+        }
+        if (C & 1)
+            for (int a = tid; a < 3; a += PX_NT) {
+                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
+            }
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
+    } else {
+        for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
+    }
     const bool constrained = __syncthreads_or(cst);
     if (tid == 0) {   // ViennaRNA's S1 wrap-around
         L.S[0] = L.S[N];
@@ -400,26 +453,17 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const float mext = XS->motif_extra;
     const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
 
-    // every cell, one flat pass: inner code; changed cells: the hairpin (+ motif)
-    // initial value (pairable) or the mark, the multiloop stem in qm1 (F reads
-    // both before overwriting); unchanged cells and q5 from the current tables
-    for (int k = tid; k < C; k += PX_NT) {
-        int D = 4;
-        {   // diagonal of the diagonal-major index k
-            const float b = float(2 * N - 7);
-            D = 4 + int((b - sqrtf(fmaxf(b * b - 8.f * float(k), 0.f))) * 0.5f);
-            D = D < 4 ? 4 : D;
-            while (D < N - 1 && off(D + 1, N) <= k) D++;
-            while (D > 4 && off(D, N) > k) D--;
-        }
-        const int i = k - off(D, N) + 1, j = i + D;
-        const int type = ptype(S[i], S[j]);
-        L.cc[k] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
-        const int rq = rowb(i, N) + D - 4, r1 = colb(j) + i - 1;
-        if (incr && (i < clo(D) || i > chi(D))) {
-            L.qb[k] = f2{src[k], src[B1 + k]};
-            L.q1[r1] = f2{src[2 * Cs + r1], src[B1 + 2 * Cs + r1]};
-        } else {
+    // cells by diagonal (wave w: diagonals 4 + w, 4 + w + NW, ...; lanes = i): the
+    // inner code of every cell; the changed cells' hairpin (+ motif) initial value
+    // (pairable) or the mark, and multiloop stem in qm1 (F reads both before it
+    // overwrites them); in a refold every other cell was restored above
+    for (int D = 4 + wid; D <= N - 1; D += PX_NW) {
+        const int od = off(D, N), lo = clo(D), hi = chi(D);
+        for (int i = 1 + lane; i <= N - D; i += WAVE) {
+            const int j = i + D;
+            const int type = ptype(S[i], S[j]);
+            L.cc[od + i - 1] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
+            if (i < lo || i > hi) continue;
             const bool pr = type != 0 && px_allowed(L, i, j);
             f2 init = f2{-0.f, -0.f};
             float m1 = 0.f;
@@ -440,17 +484,11 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 init = f2{(mx && hol0) ? h + mext : h, (mx && hol1) ? h + mext : h};
                 m1 = L.dt[DT_MLS + type * 25 + S[i - 1] * 5 + S[j + 1]];
             }
-            L.qb[k] = init;
-            L.q1[r1] = f2{m1, m1};
+            L.qb[od + i - 1] = init;
+            L.q1[colb(j) + i - 1] = f2{m1, m1};
         }
-        // qm: unchanged items from src (changed ones are written by M)
-        if (incr && D <= N - 3 && (i < qlo(D) || i > qhi(D))) L.qm[rq] = f2{src[Cs + rq], src[B1 + Cs + rq]};
-        else L.qm[rq] = f2{0.f, 0.f};
     }
-    for (int k = tid; k <= N; k += PX_NT) {
-        if (incr && k <= m_lo - 2) {
-            L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
-        } else if (k <= 3) {   // q5[0..3] (pf_group: unpaired prefix)
+    for (int k = tid; k <= 3 && k <= N; k += PX_NT) {   // q5[0..3] (pf_group: unpaired prefix)
             float q = 1.f;
             bool ok = true;
             for (int t = 1; t <= k; t++) {
@@ -458,69 +496,139 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 q *= sig1;
             }
             L.q5[k] = ok ? f2{q, q} : f2{0.f, 0.f};
+    }
+    __syncthreads();
+    // rank lists of the changed pairable cells per diagonal (the B lanes; the mark
+    // is final after the pass above): cl[off(D) + rank] = i, cn[D] = count
+    for (int D = 4 + wid; D <= N - 1; D += PX_NW) {
+        const int od = off(D, N), lo = clo(D), hi = chi(D);
+        int base = 0;
+        for (int i0 = lo; i0 <= hi; i0 += WAVE) {
+            const int i = i0 + lane;
+            const bool pr = i <= hi && !is_mark2(L.qb[od + i - 1]);
+            const uint64_t m = __ballot(pr);
+            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            if (pr) L.cl[od + slot] = uint8_t(i);
+            base += __popcll(m);
         }
+        if (lane == 0) L.cn[D] = uint8_t(base);
     }
     __syncthreads();
     PSTAMP(0);
 
-    // ---- records (wave 13): compaction of the changed pairable cells of
-    // diagonal D and their setup values (outer factors of the closing pair, the
-    // 1x1..2x2 table factors, the unpaired runs), written at step D - 1
-    auto rec_make = [&](int D) {
-        if (D < 6 || D > N - 1) {
-            if (lane == 0) L.rcnt[D & 1] = 0;
-            return;
-        }
-        const int lo = clo(D), hi = chi(D);
-        int base = 0;
-        for (int i0 = lo; i0 <= hi; i0 += WAVE) {
-            const int i = i0 + lane;
-            const bool pr = i <= hi && !is_mark2(L.qb[off(D, N) + i - 1]);
-            const uint64_t m = __ballot(pr);
-            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-            if (pr) L.cl[slot] = uint8_t(i);
-            base += __popcll(m);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int umax = min(30, D - 6);
-        for (int k = 0; k * WAVE < base; k++) {
-            const int idx = k * WAVE + lane;
-            const bool v = idx < base;
-            const int i = v ? L.cl[idx] : int(L.cl[0]), j = i + D;
-            const int ty = ptype(S[i], S[j]);
-            const int si1 = S[i + 1], sj1 = S[j - 1];
-            const int oc = ty * 25 + si1 * 5 + sj1;
-            const int A = L.up[i + 1], Bq = L.dn[j - 1];
-            float t11 = 0.f, t12 = 0.f, t21 = 0.f, t22 = 0.f;
-            // kernels.hip load_chunk: lane-4c+g table factors, here per cell
-            auto t2of = [&](int n1, int n2) { return (L.cc[off(D - 2 - n1 - n2, N) + i + n1] * 41) >> 10; };
-            if (umax >= 2) t11 = T.int11[ty][t2of(1, 1)][si1][sj1];
-            if (umax >= 3) {
-                t12 = T.int21[ty][t2of(1, 2)][si1][S[j - 2]][sj1];
-                t21 = T.int21[t2of(2, 1)][ty][sj1][si1][S[i + 2]];
-            }
-            if (umax >= 4) t22 = T.int22[ty][t2of(2, 2)][si1][S[i + 2]][S[j - 2]][sj1];
-            const float mmo = L.dt[DT_MMI + oc];
-            float *r = L.rec + (((D & 1) * 2 + k) * PX_RF) * WAVE + lane;
-            const bool mkc = A < umax || Bq < umax;
-            r[0] = __int_as_float(i);
-            r[WAVE] = __int_as_float(ty | (A << 8) | (Bq << 16) | (mkc ? (1 << 24) : 0) | (v ? (1 << 25) : 0));
-            r[2 * WAVE] = mmo;
-            r[3 * WAVE] = ty > 2 ? eTAU : 1.f;
-            r[4 * WAVE] = ct[CT_ONEN + oc] * mmo;
-            r[5 * WAVE] = ct[CT_M23O + oc];
-            r[6 * WAVE] = t11;
-            r[7 * WAVE] = t12;
-            r[8 * WAVE] = t21;
-            r[9 * WAVE] = t22;
-        }
-        if (lane == 0) L.rcnt[D & 1] = base;
+    // ---- records (wave 13): the changed pairable cells of diagonal D (rank
+    // lists) and their setup values -- outer factors of the closing pair, the
+    // unpaired runs, the 1x1..2x2 table factors (HBM/L2 loads) -- gathered at step
+    // D - 2 (rec_load) and written at step D - 1 (rec_store), so the table loads
+    // complete in the shadow of a step
+    struct Pend {
+        int n;                       // cells
+        int i[2], w1[2];             // per lane-set: i, ty | A << 8 | B << 16 | flags
+        float mmo[2], tau[2], mo[2], m23[2], t11[2], t12[2], t21[2], t22[2];
     };
-    if (wid == PX_NW - 1) rec_make(4);   // the sweep's first B diagonal (no loop fits: count 0)
+    struct Seq {                     // per lane-set: i and the bases around the closing pair
+        int n;
+        int i[2], sq[2];             // sq: ty | si1 << 4 | sj1 << 8 | si2 << 12 | sj2 << 16 | A << 20 (A, B: 6 bits)
+        int ab[2];                   // A | B << 8
+    };
+    // three stages a step apart: seq_load (rank list, bases), rec_load (tables:
+    // LDS factors, HBM/L2 1x1..2x2 factors), rec_store -- one LDS round trip each
+    auto seq_load = [&](int D) {
+        Seq Q;
+        Q.n = 0;
+        if (D < 6 || D > N - 1) return Q;
+        const int od = off(D, N);
+        Q.n = uni(L.cn[D]);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (k * WAVE >= Q.n) break;
+            const int idx = k * WAVE + lane;
+            const int i = L.cl[od + (idx < Q.n ? idx : 0)], j = i + D;
+            Q.i[k] = i;
+            Q.sq[k] = ptype(S[i], S[j]) | (S[i + 1] << 4) | (S[j - 1] << 8) | (S[i + 2] << 12) | (S[j - 2] << 16);
+            Q.ab[k] = L.up[i + 1] | (L.dn[j - 1] << 8);
+        }
+        return Q;
+    };
+    auto rec_load = [&](int D, const Seq &Q) {
+        Pend P;
+        P.n = Q.n;
+        const int umax = min(30, D - 6);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (k * WAVE >= Q.n) break;
+            const bool v = k * WAVE + lane < Q.n;
+            const int i = Q.i[k], sqk = Q.sq[k];
+            const int ty = sqk & 15, si1 = (sqk >> 4) & 15, sj1 = (sqk >> 8) & 15, si2 = (sqk >> 12) & 15,
+                      sj2 = (sqk >> 16) & 15;
+            const int oc = ty * 25 + si1 * 5 + sj1;
+            const int A = Q.ab[k] & 255, Bq = Q.ab[k] >> 8;
+            P.t11[k] = P.t12[k] = P.t21[k] = P.t22[k] = 0.f;
+            {   // kernels.hip load_chunk: the table factors of the 1x1..2x2 loops
+                auto t2of = [&](int n1, int n2) { return (L.cc[off(D - 2 - n1 - n2, N) + i + n1] * 41) >> 10; };
+                if (umax >= 2) P.t11[k] = T.int11[ty][t2of(1, 1)][si1][sj1];
+                if (umax >= 3) {
+                    P.t12[k] = T.int21[ty][t2of(1, 2)][si1][sj2][sj1];
+                    P.t21[k] = T.int21[t2of(2, 1)][ty][sj1][si1][si2];
+                }
+                if (umax >= 4) P.t22[k] = T.int22[ty][t2of(2, 2)][si1][si2][sj2][sj1];
+            }
+            const bool mkc = A < umax || Bq < umax;
+            P.i[k] = i;
+            P.w1[k] = ty | (A << 8) | (Bq << 16) | (mkc ? (1 << 24) : 0) | (v ? (1 << 25) : 0);
+            P.mmo[k] = L.dt[DT_MMI + oc];
+            P.tau[k] = ty > 2 ? eTAU : 1.f;
+            P.mo[k] = ct[CT_ONEN + oc] * P.mmo[k];
+            P.m23[k] = ct[CT_M23O + oc];
+        }
+        return P;
+    };
+    auto rec_store = [&](int D, const Pend &P) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (k * WAVE >= P.n) break;
+            float *r = L.rec + (((D & 1) * 2 + k) * PX_RF) * WAVE + lane;
+            r[0] = __int_as_float(P.i[k]);
+            r[WAVE] = __int_as_float(P.w1[k]);
+            r[2 * WAVE] = P.mmo[k];
+            r[3 * WAVE] = P.tau[k];
+            r[4 * WAVE] = P.mo[k];
+            r[5 * WAVE] = P.m23[k];
+            r[6 * WAVE] = P.t11[k];
+            r[7 * WAVE] = P.t12[k];
+            r[8 * WAVE] = P.t21[k];
+            r[9 * WAVE] = P.t22[k];
+        }
+        if (lane == 0) L.rcnt[D & 1] = P.n;
+    };
+    Pend pend;
+    Seq seqp;
+    if (wid == PX_NW - 1) {
+        rec_store(4, rec_load(4, seq_load(4)));   // the sweep's first B diagonal (no loop fits: count 0)
+        pend = rec_load(5, seq_load(5));
+        seqp = seq_load(6);
+    }
     __syncthreads();
 
+    // Q: exterior-stem factors of column j (cells (k, j), k <= j - 4, two lane-sets):
+    // INVMM(code) * ext(type, S[k-1], S[j+1]) -- static, gathered a step ahead
+    float qf[2] = {0.f, 0.f};
+    auto qfac = [&](int j) {
+        if (j < 4 || j > N) return;
+        const int sjp = (j < N) ? S[j + 1] : 5;
+        const int sj = S[j];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int kk = 1 + h * WAVE + lane;
+            const bool ok = kk <= j - 4;
+            const int k = ok ? kk : 1;
+            const int ix = off(j - k, N) + k - 1;
+            const int ty = ptype(S[k], sj);
+            const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? S[k - 1] : 5) * 6 + sjp];
+            qf[h] = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
+        }
+    };
+    if (wid == PX_NB + PX_NMW + 1) qfac(4);
     const int s_end = N + 1;
     if (wid < PX_NB) {
         switch (wid) {
@@ -536,24 +644,28 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             default: pb_sweep<16, 13, 15, 14>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
     } else {
+        // the M / F / Q / R chains set the step time; issue arbitration favours the
+        // older (B) waves of the workgroup, so these run at a higher priority
+        __builtin_amdgcn_s_setprio(2);
         for (int s = 4; s <= s_end; s++) {
             if (wid < PX_NB + PX_NMW) {
-                // ---------------- M: qm items of span sq = s - 2, K lanes per item
-                // (power of two, items x K <= the M waves' lanes), split points in
-                // contiguous runs per lane, summed over the K lanes:
+                // ---------------- M: qm items of span sq = s - 2, K lanes per item (a
+                // power of two <= 16, one DPP row), split points in contiguous runs per
+                // lane, summed over the K lanes:
                 //   qm(i, jb)  = sum_t [t <= up_i] pw(t) qm1(i+t, jb) + sum_{t >= 5} qm(i, i+t-1) qm1(i+t, jb)
                 //   mla(i, sq) = the split part
+                // K follows the full fold's item count N - sq, so a refold sums every
+                // item in the order a fold from scratch does (bit-identical tables)
                 const int sq = s - 2;
                 if (sq >= 4 && sq <= N - 3) {
                     const int lo = qlo(sq), n = qhi(sq) - lo + 1;
-                    // K from the full fold's item count: a refold sums every item in
-                    // the same order as a fold from scratch (bit-identical tables)
                     int K = 16;
                     while (K > 1 && (N - sq) * K > PX_NMW * WAVE) K >>= 1;
                     const int ipw = WAVE / K;                 // items per wave
                     const int mw = wid - PX_NB;
+                    const int k = lane & (K - 1);
+                    const int item = mw * ipw + lane / K;
                     if (mw * ipw < n) {
-                        const int item = mw * ipw + lane / K, k = lane & (K - 1);
                         const bool valid = item < n;
                         const int i = lo + (valid ? item : n - 1);
                         const int jb = i + sq, T = sq - 4;
@@ -563,32 +675,32 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         const f2 *pq = L.q1 + colb(jb) + i - 1;   // qm1(i+t, jb) at +t
                         const f2 *pr = L.qm + rowb(i, N) - 5;      // qm(i, i+t-1) at +t (t >= 5)
                         f2 A = {0.f, 0.f}, A1 = {0.f, 0.f}, Pp = {0.f, 0.f};
+                        float wt = L.pw[t0];                   // pw(t) = pw(t0) (expMLbase sigma)^(t - t0)
                         for (int t = t0; t <= t1; t += 8) {
                             f2 qv[8], rv[8];
-                            float wv[8];
 #pragma unroll
                             for (int kk = 0; kk < 8; kk++) {
                                 qv[kk] = pq[t + kk];
                                 rv[kk] = pr[(t + kk >= 5) ? t + kk : 5];
-                                wv[kk] = L.pw[t + kk];
                             }
 #pragma unroll
                             for (int kk = 0; kk < 8; kk++) {
                                 const int tt = t + kk;
                                 const f2 q = tt <= t1 ? qv[kk] : f2{0.f, 0.f};
-                                Pp = fma2(sp2(tt <= upi ? wv[kk] : 0.f), q, Pp);
+                                Pp = fma2(sp2(tt <= upi ? wt : 0.f), q, Pp);
+                                wt *= mlbase_sig;
                                 if (kk & 1) A1 = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A1);
                                 else A = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A);
                             }
                         }
                         A += A1;
-                        for (int o = 1; o < K; o <<= 1) {
-                            A.x += __shfl_xor(A.x, o, WAVE);
-                            A.y += __shfl_xor(A.y, o, WAVE);
-                            Pp.x += __shfl_xor(Pp.x, o, WAVE);
-                            Pp.y += __shfl_xor(Pp.y, o, WAVE);
-                        }
-                        if (valid && k == 0) {
+                        // sum over the item's K lanes (DPP within a row of 16; the
+                        // total lands in lane 0 of the item for K <= 4, lane K-1 above)
+                        if (K >= 2) { A = dpp_add2<0xb1>(A); Pp = dpp_add2<0xb1>(Pp); }     // quad_perm [1,0,3,2]
+                        if (K >= 4) { A = dpp_add2<0x4e>(A); Pp = dpp_add2<0x4e>(Pp); }     // quad_perm [2,3,0,1]
+                        if (K >= 8) { A = dpp_add2<0x114>(A); Pp = dpp_add2<0x114>(Pp); }   // row_shr:4
+                        if (K >= 16) { A = dpp_add2<0x118>(A); Pp = dpp_add2<0x118>(Pp); }  // row_shr:8
+                        if (valid && k == (K >= 8 ? K - 1 : 0)) {
                             L.qm[rowb(i, N) + sq - 4] = A + Pp;
                             L.mla[(sq & 1) * NP + i] = A;
                         }
@@ -628,32 +740,29 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     }
                 }
             } else if (wid == PX_NB + PX_NMW + 1) {
-                // ---------------- Q: q5[j], j = s - 1 (column j is final)
+                // ---------------- Q: q5[j], j = s - 1 (column j is final); the
+                // exterior factors of column j + 1 are gathered one step ahead
                 const int j = s - 1;
                 if (j >= 4 && j <= N && (!incr || j >= m_lo - 1)) {
-                    const int sjp = (j < N) ? S[j + 1] : 5;
-                    const int sj = S[j];
                     f2 acc = {0.f, 0.f};
-                    for (int k0 = 1; k0 <= j - 4; k0 += WAVE) {
-                        const int kk = k0 + lane;
-                        const bool ok = kk <= j - 4;
-                        const int k = ok ? kk : 1;
-                        const int ix = off(j - k, N) + k - 1;
-                        const int ty = ptype(S[k], sj);
-                        const float e = L.dt[DT_EXT + ty * 36 + ((k > 1) ? S[k - 1] : 5) * 6 + sjp];
-                        const float f = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
-                        acc = fma2(L.q5[k - 1] * L.qb[ix], sp2(f), acc);
-                    }
 #pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) {
-                        acc.x += __shfl_xor(acc.x, o, WAVE);
-                        acc.y += __shfl_xor(acc.y, o, WAVE);
+                    for (int h = 0; h < 2; h++) {
+                        if (h * WAVE >= j - 4) break;
+                        const int kk = 1 + h * WAVE + lane;
+                        const int k = kk <= j - 4 ? kk : 1;
+                        const int ix = off(j - k, N) + k - 1;
+                        acc = fma2(L.q5[k - 1] * L.qb[ix], sp2(qf[h]), acc);
                     }
+                    acc = wave_sum_f2(acc);
                     if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sp2(sig1) : f2{0.f, 0.f}) + acc;
                 }
+                qfac(j + 1);
             } else if (wid == PX_NW - 1) {
-                // ---------------- R: records of diagonal s + 1 (next step's B)
-                rec_make(s + 1);
+                // ---------------- R: records of diagonal s + 1 (next step's B), tables of
+                // s + 2, bases of s + 3
+                rec_store(s + 1, pend);
+                pend = rec_load(s + 2, seqp);
+                seqp = seq_load(s + 3);
             }
             PSTAMP(4);
             lds_barrier();

@@ -145,6 +145,15 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
             "reference_2016_per_core": 14.4}
 
 
+def pf_kernel_label(bppm):
+    """The PF kernels of one step's score window (kernels.hip launch_score_m / launch_steps)."""
+    inside = ("score_kernel<SumProd> (lanes = terms)" if os.environ.get("ADX_PF_KERNEL") == "rows"
+              else "pf_cells_kernel (lanes = cells)")
+    if bppm:
+        return inside + " + outside_cells_kernel + combine_kernel (one event window per step)"
+    return inside + " + combine_kernel"
+
+
 def mfe_kernel_label():
     """The MFE fold kernel the engine launches (kernels.hip mfe_kernel_choice)."""
     k = os.environ.get("ADX_MFE_KERNEL", "cells")
@@ -254,9 +263,9 @@ def main():
     f_free = sum(work(s, None) for s in sample) / len(sample)
     f_act = sum(work(s, active) for s in sample) / len(sample)
     flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
-    if a.bppm:   # bppm_kernel: inside + outside of the apo and holo unconstrained folds
+    if a.bppm:   # outside passes of the apo and holo unconstrained folds (on the stored inside tables)
         f_out = sum(roofline.outside_flops(s, None) for s in sample) / len(sample)
-        flop_per_scored += 2 * (f_free + f_out)
+        flop_per_scored += 2 * f_out
     launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
     achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
     # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
@@ -283,8 +292,7 @@ def main():
         "frac": (achieved_tflops / peak) if achieved_tflops else None,
         "traffic": traffic,
         "compute_unit": peak_note,
-        "kernel": ("bppm_kernel + score_kernel<SumProd> (one event window per step)" if a.bppm
-                   else mfe_kernel_label() if a.fold == "mfe" else "score_kernel<SumProd>"),
+        "kernel": mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(a.bppm),
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": score_ms,
         "launches": launches,

@@ -210,7 +210,8 @@ def test_mc_large_batch_invariants(native, oracle):
 
 def test_mc_pf_incremental_consistency(native, oracle):
     """Incremental refolds (stored tables + changed cells) give the scores a
-    from-scratch fold gives: 1024 walkers x 40 steps, then adx_score_batch."""
+    from-scratch fold gives: 1024 walkers x 40 steps, then adx_score_batch
+    (every kernel sums a cell in the same order in both: bit-identical)."""
     tmpl, active = workloads.synthetic(100)
     terms = workloads.default_objective()
     th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)

@@ -15,9 +15,9 @@ import csv
 import json
 import sys
 
-# the kernels of one step's score window (kernels.hip, mfe_cells.hip, outside_cells.hip):
+# the kernels of one step's score window (kernels.hip, mfe_cells.hip, pf_cells.hip, outside_cells.hip):
 # the fold kernels, and with pair terms the outside pass and the score combine
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "outside_cells_kernel", "bppm_kernel", "combine_kernel")
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "pf_cells_kernel", "outside_cells_kernel", "bppm_kernel", "combine_kernel")
 
 
 def per_kernel(path, counter):

@@ -15,7 +15,7 @@ import json
 import sys
 
 # the fold kernels one score launch consists of (kernels.hip, mfe_cells.hip)
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel")
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "pf_cells_kernel")
 
 path = sys.argv[1]
 last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 10
