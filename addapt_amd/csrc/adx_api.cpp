@@ -871,6 +871,7 @@ struct adx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
     double score_ms_total = 0.0;   // sum of the score-kernel launch durations of the last run
+    double inside_ms_total = 0.0, outside_ms_total = 0.0;   // the same windows split (inside, outside)
     int score_launches = 0;
 
     ~adx_ctx() {
@@ -1247,8 +1248,8 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
         st.tr_u = tu.p;
         st.tr_terms = ntt > 0 ? tterms.p : nullptr;
     }
-    // events around every score launch (the dominant kernel) for its average duration
-    std::vector<hipEvent_t> evs(2 * size_t(steps));
+    // events around every score window (the dominant kernels) for its average duration
+    std::vector<hipEvent_t> evs(4 * size_t(steps));
     for (auto &e : evs) HIP_TRY(hipEventCreate(&e));
     struct EvFree {
         std::vector<hipEvent_t> &v;
@@ -1264,13 +1265,19 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last_ms = ms;
-    double sk = 0.0;
+    double sk = 0.0, si = 0.0, so = 0.0;
     for (int k = 0; k < steps; k++) {
-        float e = 0.f;
-        HIP_TRY(hipEventElapsedTime(&e, evs[2 * k], evs[2 * k + 1]));
+        float e = 0.f, a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&e, evs[4 * k], evs[4 * k + 3]));
+        HIP_TRY(hipEventElapsedTime(&a, evs[4 * k], evs[4 * k + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, evs[4 * k + 1], evs[4 * k + 2]));
         sk += e;
+        si += a;
+        so += b;
     }
     c->score_ms_total = sk;
+    c->inside_ms_total = si;
+    c->outside_ms_total = so;
     c->score_launches = steps;
     c->step += steps;
     std::vector<int> errs(W);
@@ -1305,6 +1312,14 @@ extern "C" adx_status adx_last_score_kernel_ms(const adx_ctx *c, double *avg_ms,
     if (!c || !avg_ms) return fail(ADX_EINVAL, "adx_last_score_kernel_ms: null argument");
     *avg_ms = c->score_launches ? c->score_ms_total / c->score_launches : 0.0;
     if (launches) *launches = c->score_launches;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_last_kernel_split_ms(const adx_ctx *c, double *inside_ms, double *outside_ms) {
+    if (!c || !inside_ms || !outside_ms) return fail(ADX_EINVAL, "adx_last_kernel_split_ms: null argument");
+    const int n = c->score_launches;
+    *inside_ms = n ? c->inside_ms_total / n : 0.0;
+    *outside_ms = n ? c->outside_ms_total / n : 0.0;
     return ADX_OK;
 }
 

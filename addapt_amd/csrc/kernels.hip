@@ -2037,7 +2037,8 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
 }
 
-// evs (optional): 2 * nsteps events recorded around each step's score launch
+// evs (optional): 4 * nsteps events per step: window start, after the inside
+// folds, after the outside pass, window end (score written)
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
     for (int s = 0; s < st.nsteps; s++) {
@@ -2045,7 +2046,7 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
         // the event window covers the outside pass too when the terms read base-pair
         // probabilities (bench.py divides bppm + score work by it)
-        if (evs) (void)hipEventRecord(evs[2 * s], stream);
+        if (evs) (void)hipEventRecord(evs[4 * s], stream);
         hipError_t e;
         if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
             // inside folds first (they write the proposal's tables), then the outside
@@ -2054,6 +2055,7 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
             ki.pair_p = nullptr;
             e = launch_score_m(ki, st.prop_seq, st.W, st.prop_score, nullptr, ka.gstep, st.changed, stream);
             if (e != hipSuccess) return e;
+            if (evs) (void)hipEventRecord(evs[4 * s + 1], stream);
             // lanes = cells outside kernel (outside_cells.hip) where it covers the
             // length, else bppm_kernel on the same stored tables
             const char *ok = std::getenv("ADX_OUTSIDE_KERNEL");
@@ -2064,6 +2066,7 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
                     : launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
                                     ka.bppm_scratch, stream, true);
             if (e != hipSuccess) return e;
+            if (evs) (void)hipEventRecord(evs[4 * s + 2], stream);
             hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, st.changed,
                                st.prop_score, tv);
             e = hipGetLastError();
@@ -2074,8 +2077,12 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
                 if (e != hipSuccess) return e;
             }
             e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
+            if (evs) {
+                (void)hipEventRecord(evs[4 * s + 1], stream);
+                (void)hipEventRecord(evs[4 * s + 2], stream);
+            }
         }
-        if (evs) (void)hipEventRecord(evs[2 * s + 1], stream);
+        if (evs) (void)hipEventRecord(evs[4 * s + 3], stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,
                            ka.tab ? ka.cur_slot : nullptr);

@@ -72,6 +72,7 @@ EXPORTS = [
     "adx_eval_structure", "adx_fold_create", "adx_fold_add_motif", "adx_fold_add_constraint",
     "adx_fold_pf", "adx_fold_mfe", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
     "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
+    "adx_last_kernel_split_ms",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
     "adx_walkers_import", "adx_set_temperature", "adx_bppm_batch",
 ]
@@ -106,6 +107,7 @@ def lib():
         L.adx_run_steps.argtypes = [C.c_void_p, C.c_int, C.POINTER(Trace)]
         L.adx_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         L.adx_last_score_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+        L.adx_last_kernel_split_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.adx_walkers_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_walkers_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_set_temperature.argtypes = [C.c_void_p, C.c_double]
@@ -348,6 +350,12 @@ class Engine:
         ms, n = C.c_double(), C.c_int()
         _check(lib().adx_last_score_kernel_ms(self.ptr, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def last_kernel_split_ms(self):
+        """(average inside-fold ms, average outside-pass ms) per step of the last run_steps."""
+        a, b = C.c_double(), C.c_double()
+        _check(lib().adx_last_kernel_split_ms(self.ptr, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def download(self):
         W = self.W

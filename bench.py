@@ -248,7 +248,8 @@ def main():
     barrier()
     t1 = time.perf_counter()
     kernel_ms = eng.last_kernel_ms()            # whole timed run_steps (3 kernels per step)
-    score_ms, launches = eng.last_score_kernel_ms()   # dominant kernel, per launch
+    score_ms, launches = eng.last_score_kernel_ms()   # the step's score window, per launch
+    inside_ms, outside_ms = eng.last_kernel_split_ms()   # the same window split per kernel
     _, _, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device="cuda" if dist is not None else None)
     steps_total = W * a.steps * world
@@ -262,12 +263,18 @@ def main():
     work = roofline.pf_flops if a.fold == "pf" else roofline.mfe_ops
     f_free = sum(work(s, None) for s in sample) / len(sample)
     f_act = sum(work(s, active) for s in sample) / len(sample)
-    flop_per_scored = 2 * f_free + 2 * f_act       # apo/holo x free/active
+    flop_inside = 2 * f_free + 2 * f_act           # apo/holo x free/active
+    flop_per_scored = flop_inside
+    f_out = 0.0
     if a.bppm:   # outside passes of the apo and holo unconstrained folds (on the stored inside tables)
-        f_out = sum(roofline.outside_flops(s, None) for s in sample) / len(sample)
-        flop_per_scored += 2 * f_out
-    launch_flops = scored * flop_per_scored / max(1, a.steps)       # per score launch (one per step)
-    achieved_tflops = launch_flops / (score_ms * 1e-3) / 1e12 if score_ms > 0 else None
+        f_out = 2 * sum(roofline.outside_flops(s, None) for s in sample) / len(sample)
+        flop_per_scored += f_out
+    scored_pl = scored / max(1, a.steps)                             # scored walkers per launch
+    launch_flops = scored_pl * flop_per_scored                      # per score window (one per step)
+    # the dominant kernel's own time: the outside pass with --bppm, else the window
+    # (inside folds + the score combine)
+    kern_ms, kern_flops = (outside_ms, scored_pl * f_out) if a.bppm else (score_ms, launch_flops)
+    achieved_tflops = kern_flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
     # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
     # groups x value arrays (MFE: one packed apo/holo array; PF: two) x
     # (3 cell tables + q5) x 4 B
@@ -282,6 +289,9 @@ def main():
         with open(a.traffic_json) as f:
             tj = json.load(f)
         traffic = tj.get("bytes_per_launch")
+        if a.bppm:   # the dominant kernel's own bytes (the summary holds every kernel of the window)
+            own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if "outside_cells_kernel" in name]
+            traffic = own[0] if own else None
         traffic_src = os.path.relpath(a.traffic_json, ROOT)
     peak, peak_note = roofline.valu_peak(a.fold)
     roof = {
@@ -292,9 +302,16 @@ def main():
         "frac": (achieved_tflops / peak) if achieved_tflops else None,
         "traffic": traffic,
         "compute_unit": peak_note,
-        "kernel": mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(a.bppm),
+        "kernel": ("outside_cells_kernel (events around its launch; the window also holds "
+                   + pf_kernel_label(False) + ")") if a.bppm
+                  else mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(False),
         "traffic_source": traffic_src,
-        "kernel_ms_per_launch": score_ms,
+        "kernel_ms_per_launch": kern_ms,
+        "window_ms_per_launch": score_ms,
+        "inside_ms_per_launch": inside_ms,
+        "outside_ms_per_launch": outside_ms if a.bppm else None,
+        "inside_frac": ((scored_pl * flop_inside / (inside_ms * 1e-3) / 1e12) / peak
+                        if a.bppm and inside_ms > 0 else None),
         "launches": launches,
         "all_kernels_ms_per_step": kernel_ms / a.steps,
         "flop_per_scored_step": flop_per_scored,

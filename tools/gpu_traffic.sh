@@ -2,7 +2,7 @@
 # HBM traffic per step (FETCH_SIZE / WRITE_SIZE, one counter per rocprofv3
 # pass, MI355X_MICROARCH.md HBM corrections in tools/pmc_traffic.py) of the
 # bench workloads: mfe, pf, pf + bppm at N = 100 and 150.
-# usage: tools/gpu_traffic.sh <tag>   -> gpurun_out/<tag>/traffic_latest_*.json
+# usage: [WORKLOADS="pf pf_bppm"] tools/gpu_traffic.sh <tag>   -> gpurun_out/<tag>/traffic_latest_*.json
 set -e
 tag=${1:-traffic}
 D=gpurun_out/$tag
@@ -14,7 +14,12 @@ run() {   # name, bench args
   timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $D/$n/w -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $D/$n.write.log 2>&1
   python tools/pmc_traffic.py $(find $D/$n/f -name "*counter_collection.csv") $(find $D/$n/w -name "*counter_collection.csv") > $D/traffic_latest_$n.json
 }
-run mfe
-run pf --fold pf
-run pf_bppm --bppm
-run pf_bppm_n150 --bppm --length 150
+W=${WORKLOADS:-"mfe pf pf_bppm pf_bppm_n150"}
+for n in $W; do
+  case $n in
+    mfe) run mfe ;;
+    pf) run pf --fold pf ;;
+    pf_bppm) run pf_bppm --bppm ;;
+    pf_bppm_n150) run pf_bppm_n150 --bppm --length 150 ;;
+  esac
+done
