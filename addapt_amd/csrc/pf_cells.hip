@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 
 #include "dev_types.hpp"
@@ -213,6 +214,58 @@ struct PxSize {
     }
 };
 
+// Loop size U >= 6 over the four lanes of a cell (phase r = lane & 3): lane r
+// takes one of the four special shapes -- bulges (0,U) (U,0), 1 x n loops
+// (1,U-1) (U-1,1) -- and the generic shapes n1 = 2 + r, 6 + r, ... <= U - 2
+// (one read at a per-lane base + immediate offset 4m, its factor in a VGPR;
+// 0 past the size, so the last round needs no mask).  Every lane runs the same
+// code; the four lanes' sums are added in a fixed order (bit-identical refolds).
+template <int U>
+struct PxSizeQ {
+    static constexpr int NR = U >= 6 ? (U - 3 + 3) / 4 : 1;   // generic rounds
+    float gf[NR];
+    float fsp;      // the lane's special-shape factor (bulge FB[U] or 1 x n F1N[U-1])
+    int n1sp;       // the lane's special shape
+    __device__ __forceinline__ void load(const DevScaled *XS, int r) {
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const int n1 = 2 + 4 * m + r;
+            gf[m] = n1 <= U - 2 ? XS->fgen[(U - 6) * FG_ROW + n1 - 2] : 0.f;
+        }
+        n1sp = r == 0 ? 0 : r == 1 ? U : r == 2 ? 1 : U - 1;
+        fsp = r < 2 ? XS->ctab[CT_FB + U] : XS->ctab[CT_F1N + U - 1];
+    }
+    template <bool MK>
+    __device__ __forceinline__ void run(const PxL &L, const PxCell &c, int s, int umax, int r, int ctb, float outer,
+                                        f2 &g, f2 &sp) const {
+        if (U <= umax) {
+            const int o = off(s - 2 - U, L.N) + c.i;   // inner cell (i+1+n1, ...) at o + n1
+            uint32_t bits = ~0u;
+            if constexpr (MK) {   // n1 <= A and U - n1 <= B
+                const int lo = max(0, U - c.B), hi = min(U, c.A);
+                bits = hi < lo ? 0u : ((2u << hi) - 1u) & ~((1u << lo) - 1u);
+            }
+            // special shape of this lane
+            {
+                f2 v = L.qb[o + n1sp];
+                if constexpr (MK) v *= sp2(float((bits >> n1sp) & 1u));
+                const int ci = L.cc[o + n1sp];
+                sp = fma2(v, sp2(L.ct[ctb + ci] * (outer * fsp)), sp);
+            }
+            // generic shapes n1 = 2 + r + 4m
+            const f2 *q = L.qb + o + 2 + r;
+            const uint32_t bm = bits >> (2 + r);
+#pragma unroll
+            for (int m = 0; m < NR; m++) {
+                f2 v = q[4 * m];
+                if constexpr (MK) v *= sp2(float((bm >> (4 * m)) & 1u));
+                g.x = fmaf(v.x, gf[m], g.x);
+                g.y = fmaf(v.y, gf[m], g.y);
+            }
+        }
+    }
+};
+
 #ifdef ADX_STAMP
 __device__ unsigned long long g_stamps_p[16][8];
 #define PSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -224,64 +277,103 @@ __device__ unsigned long long g_stamps_p[16][8];
 #define PX_STP_ARGS
 #endif
 
-// B: interior-loop sums of every diagonal for one block of loop sizes, the
-// block's shape factors in registers for the whole sweep; writes the partial
-// of each compacted pairable cell to its natural slot.
-template <int U0, int U1, int U2, int U3>
+// B: interior-loop sums of every diagonal for one block of loop sizes.  Lanes
+// = (cell, phase r): four lanes per cell (16 cells per lane-set), sizes >= 6 as
+// PxSizeQ (shapes spread over the phases), sizes <= 5 (the stack, 1x1..2x3
+// table loops) computed whole by every lane and counted once (phase 0).  The
+// four partials are summed by DPP and phase 0 writes the cell's natural slot.
+template <int U>
+struct PxBlk {   // the size's state in a B wave
+    using T = typename std::conditional<(U < 0), PxSize<-1>, typename std::conditional<(U <= 5), PxSize<U>, PxSizeQ<U>>::type>::type;
+};
+template <int U, bool MK>
+__device__ __forceinline__ void px_run(const typename PxBlk<U>::T &z, const PxL &L, const PxCell &c, int s, int umax,
+                                       int r, int ctb, float outer, f2 &g, f2 &sp, f2 &gs, f2 &sps) {
+    if constexpr (U < 0) {
+    } else if constexpr (U <= 5) {
+        z.template run<MK>(L, c, s, umax, gs, sps);
+    } else {
+        z.template run<MK>(L, c, s, umax, r, ctb, outer, g, sp);
+    }
+}
+template <int U>
+__device__ __forceinline__ void px_load(typename PxBlk<U>::T &z, const DevScaled *XS, int r) {
+    if constexpr (U < 0) {
+    } else if constexpr (U <= 5) {
+        z.load(XS, 0);   // uniform factors: SGPRs
+    } else {
+        z.load(XS, r);
+    }
+}
+__device__ __forceinline__ f2 quad_sum(f2 v) {   // sum over the 4 lanes of a quad, in every lane
+    v = dpp_add2<0xb1>(v);   // quad_perm [1,0,3,2]
+    return dpp_add2<0x4e>(v);   // quad_perm [2,3,0,1]
+}
+
+template <int U0, int U1, int U2, int U3, int U4>
 __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int N, int lane, int wid,
                                          bool constrained, int s_end PX_STP_PARAMS) {
-    constexpr bool TB = (U0 >= 2 && U0 <= 4) || (U1 >= 2 && U1 <= 4) || (U2 >= 2 && U2 <= 4) || (U3 >= 2 && U3 <= 4);
-    PxSize<U0> s0;
-    PxSize<U1> s1;
-    PxSize<U2> s2;
-    PxSize<U3> s3;
-    // uniform factors: SGPRs (a VALU FMA reads one SGPR operand for free)
-    s0.load(XS, 0);
-    s1.load(XS, 0);
-    s2.load(XS, 0);
-    s3.load(XS, 0);
+    constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
+    constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
+    const int r = lane & 3, cq = lane >> 2;
+    typename PxBlk<U0>::T s0;
+    typename PxBlk<U1>::T s1;
+    typename PxBlk<U2>::T s2;
+    typename PxBlk<U3>::T s3;
+    typename PxBlk<U4>::T s4;
+    px_load<U0>(s0, XS, r);
+    px_load<U1>(s1, XS, r);
+    px_load<U2>(s2, XS, r);
+    px_load<U3>(s3, XS, r);
+    px_load<U4>(s4, XS, r);
+    const int ctb = r < 2 ? CT_BUL : CT_ONEN;   // the lane's special-shape inner factor table
     for (int s = 4; s <= s_end; s++) {
         const int par = s & 1;
         const int umax = min(30, s - 6);   // no interior loop fits a span below 6
-        const int ncls = (s <= N - 1 && umax >= 0) ? (uni(L.rcnt[par]) + WAVE - 1) / WAVE : 0;
-        for (int ls = 0; ls < ncls; ls++) {
-            const float *r = L.rec + ((par * 2 + ls) * PX_RF) * WAVE + lane;
-            const int fl = __float_as_int(r[WAVE]);
+        const int ncell = (s <= N - 1 && umax >= 0) ? uni(L.rcnt[par]) : 0;
+        for (int c0 = 0; c0 < ncell; c0 += WAVE / 4) {
+            const int idx = c0 + cq;   // the lane's cell (records: set idx / 64, lane idx % 64)
+            const float *rr = L.rec + ((par * 2 + (idx >> 6)) * PX_RF) * WAVE + (idx & (WAVE - 1));
+            const int fl = __float_as_int(rr[WAVE]);
             PxCell c;
-            c.i = __float_as_int(r[0]);
+            c.i = __float_as_int(rr[0]);
             c.ty8 = (fl & 7) * 8;
             c.A = (fl >> 8) & 255;
             c.B = (fl >> 16) & 255;
-            const float mmo = r[2 * WAVE];
-            c.tau = r[3 * WAVE];
-            c.mo = r[4 * WAVE];
-            c.m23 = r[5 * WAVE];
+            const float mmo = rr[2 * WAVE];
+            c.tau = rr[3 * WAVE];
+            c.mo = rr[4 * WAVE];
+            c.m23 = rr[5 * WAVE];
             c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
             if constexpr (TB) {
-                c.t11 = r[6 * WAVE];
-                c.t12 = r[7 * WAVE];
-                c.t21 = r[8 * WAVE];
-                c.t22 = r[9 * WAVE];
+                c.t11 = rr[6 * WAVE];
+                c.t12 = rr[7 * WAVE];
+                c.t21 = rr[8 * WAVE];
+                c.t22 = rr[9 * WAVE];
             }
-            f2 g = {0.f, 0.f}, sp = {0.f, 0.f};
+            const float outer = r < 2 ? c.tau : c.mo;
+            f2 g = {0.f, 0.f}, sp = {0.f, 0.f}, gs = {0.f, 0.f}, sps = {0.f, 0.f};
             PSTAMP(2);
             // shapes past a cell's allowed unpaired runs (constraints) are masked
             const bool mk = constrained && __ballot((fl >> 24) & 1) != 0;
             if (mk) {
-                s0.template run<true>(L, c, s, umax, g, sp);
-                s1.template run<true>(L, c, s, umax, g, sp);
-                s2.template run<true>(L, c, s, umax, g, sp);
-                s3.template run<true>(L, c, s, umax, g, sp);
+                px_run<U0, true>(s0, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U1, true>(s1, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U2, true>(s2, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U3, true>(s3, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U4, true>(s4, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
             } else {
-                s0.template run<false>(L, c, s, umax, g, sp);
-                s1.template run<false>(L, c, s, umax, g, sp);
-                s2.template run<false>(L, c, s, umax, g, sp);
-                s3.template run<false>(L, c, s, umax, g, sp);
+                px_run<U0, false>(s0, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U1, false>(s1, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U2, false>(s2, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U3, false>(s3, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
+                px_run<U4, false>(s4, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
             }
             PSTAMP(3);
-            if ((fl >> 25) & 1)   // a real cell (not an idle lane)
-                L.part[((par * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] =
-                    fma2(g, sp2(mmo), sp);
+            // small sizes count once (phase 0), then the cell's total over its four lanes
+            const f2 part = quad_sum(fma2(g, sp2(mmo), sp) + (r == 0 ? fma2(gs, sp2(mmo), sps) : f2{0.f, 0.f}));
+            if (r == 0 && idx < ncell && ((fl >> 25) & 1))
+                L.part[((par * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] = part;
         }
         PSTAMP(5);
         lds_barrier();
@@ -632,16 +724,16 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const int s_end = N + 1;
     if (wid < PX_NB) {
         switch (wid) {
-            // sizes U, U' with U + U' = 29 cost 31 shape reads together: two such
-            // units (or 30 alone) per wave
-            case 0: pb_sweep<30, 29, 0, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 1: pb_sweep<28, 1, 27, 2>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 2: pb_sweep<26, 3, 25, 4>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 3: pb_sweep<24, 5, 23, 6>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 4: pb_sweep<22, 7, 21, 8>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 5: pb_sweep<20, 9, 19, 10>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 6: pb_sweep<18, 11, 17, 12>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            default: pb_sweep<16, 13, 15, 14>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            // blocks of about equal LDS cost per lane-set (a size >= 6: 3 reads for
+            // its special shapes + one per 4 generic ones; the small sizes ~3 per shape)
+            case 0: pb_sweep<30, 29, 0, 1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<28, 27, 2, 6, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 2: pb_sweep<26, 25, 3, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<24, 23, 4, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<5, 7, 8, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<22, 21, 20, 9, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<19, 18, 17, 10, 11>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            default: pb_sweep<16, 15, 14, 13, 12>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
     } else {
         // the M / F / Q / R chains set the step time; issue arbitration favours the
