@@ -8,18 +8,18 @@
 //     variants of one (context, macrostate)), the two folds in lockstep as
 //     float2 (ds_read_b64, v_pk_fma_f32: one instruction serves both);
 //   * one anti-diagonal per step, ONE barrier per step.  Step s runs
-//       B   the interior-loop sums of diagonal s (waves 0-7, lanes = the
-//           changed pairable cells compacted one step ahead; shapes by loop
-//           size in blocks of equal cost, factors in registers; every shape
-//           one read of the inner cell at a per-lane base plus an immediate
-//           offset);
-//       M   the qm (fML) items of span s-2 (waves 8-10; K lanes per item so
+//       B   the interior-loop sums of diagonal s (waves 0-7, loop sizes in
+//           blocks of equal cost; four lanes per changed pairable cell, each
+//           taking a quarter of a size's shapes; every shape one read of the
+//           inner cell at a per-lane base plus an immediate offset);
+//       M   the qm (fML) items of span s-2 (waves 11-13; K lanes per item so
 //           that the few long items of late spans spread over the waves, the
 //           split points read from the row-major qm and column-major qm1 at
 //           immediate offsets);
-//       F   the cells of diagonal s-1 (wave 11): qb, qbm, qm1;
-//       Q   q5[s-1] (wave 12);
-//       R   the compaction and setup records of diagonal s+1 (wave 13).
+//       F   the cells of diagonal s-1 (wave 8): qb, qbm, qm1;
+//       Q   q5[s-1] (wave 9);
+//       R   the setup records of diagonal s+1 (wave 10), built in four
+//           stages a step apart.
 //
 // Covered: N <= 100 (LDS); longer folds take kernels.hip score_kernel.
 #include <hip/hip_runtime.h>
@@ -39,9 +39,17 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int PX_NW = 14;
 constexpr int PX_NT = PX_NW * WAVE;
 constexpr int PX_NB = 8;              // interior-loop blocks (waves 0..7)
-constexpr int PX_NMW = 3;             // qm item waves (8..10); then F (11), Q (12), records (13)
+constexpr int PX_NMW = 3;             // qm item waves
+// Roles of waves 8-13.  A workgroup's waves go to SIMDs 0, 2, 1, 3, 0, 2, ...
+// (wave w on SIMD {0,2,1,3}[w % 4]), so SIMDs 0 and 2 host two of these waves
+// and 1 and 3 one: the two heaviest chains (records, the first qm wave) get a
+// SIMD of their own, the others pair up.
+constexpr int PX_WF = 8, PX_WQ = 9, PX_WR = 10;   // F, Q, R
+__host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most items) or -1
+    return w == 11 ? 0 : w == 13 ? 1 : w == 12 ? 2 : -1;
+}
 constexpr int PX_NMAX = 100;
-constexpr int PX_RF = 10;             // record fields (rec_write)
+constexpr int PX_RF = 8;              // record fields (rec_store): word, mmo, mo, m23, 1x1..2x2 factors
 constexpr int PX_SLACK = 16;
 
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -315,6 +323,8 @@ __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int 
                                          bool constrained, int s_end PX_STP_PARAMS) {
     constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
     constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
+    constexpr bool H5 = U0 == 5 || U1 == 5 || U2 == 5 || U3 == 5 || U4 == 5;   // 2x3 loops (m23)
+    const float eTAU = XS->ctab[CT_FSM + 6];
     const int r = lane & 3, cq = lane >> 2;
     typename PxBlk<U0>::T s0;
     typename PxBlk<U1>::T s1;
@@ -334,28 +344,31 @@ __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int 
         for (int c0 = 0; c0 < ncell; c0 += WAVE / 4) {
             const int idx = c0 + cq;   // the lane's cell (records: set idx / 64, lane idx % 64)
             const float *rr = L.rec + ((par * 2 + (idx >> 6)) * PX_RF) * WAVE + (idx & (WAVE - 1));
-            const int fl = __float_as_int(rr[WAVE]);
+            // word: i | ty << 7 | A << 10 | B << 18 | masked << 26 | real << 27; a block
+            // reads only the fields its sizes use
+            const int fl = __float_as_int(rr[0]);
             PxCell c;
-            c.i = __float_as_int(rr[0]);
-            c.ty8 = (fl & 7) * 8;
-            c.A = (fl >> 8) & 255;
-            c.B = (fl >> 16) & 255;
-            const float mmo = rr[2 * WAVE];
-            c.tau = rr[3 * WAVE];
-            c.mo = rr[4 * WAVE];
-            c.m23 = rr[5 * WAVE];
+            c.i = fl & 127;
+            const int ty = (fl >> 7) & 7;
+            c.ty8 = ty * 8;
+            c.A = (fl >> 10) & 255;
+            c.B = (fl >> 18) & 255;
+            const float mmo = rr[WAVE];
+            c.tau = ty > 2 ? eTAU : 1.f;
+            c.mo = rr[2 * WAVE];
+            c.m23 = H5 ? rr[3 * WAVE] : 0.f;
             c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
             if constexpr (TB) {
-                c.t11 = rr[6 * WAVE];
-                c.t12 = rr[7 * WAVE];
-                c.t21 = rr[8 * WAVE];
-                c.t22 = rr[9 * WAVE];
+                c.t11 = rr[4 * WAVE];
+                c.t12 = rr[5 * WAVE];
+                c.t21 = rr[6 * WAVE];
+                c.t22 = rr[7 * WAVE];
             }
             const float outer = r < 2 ? c.tau : c.mo;
             f2 g = {0.f, 0.f}, sp = {0.f, 0.f}, gs = {0.f, 0.f}, sps = {0.f, 0.f};
             PSTAMP(2);
             // shapes past a cell's allowed unpaired runs (constraints) are masked
-            const bool mk = constrained && __ballot((fl >> 24) & 1) != 0;
+            const bool mk = constrained && __ballot((fl >> 26) & 1) != 0;
             if (mk) {
                 px_run<U0, true>(s0, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
                 px_run<U1, true>(s1, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
@@ -372,7 +385,7 @@ __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int 
             PSTAMP(3);
             // small sizes count once (phase 0), then the cell's total over its four lanes
             const f2 part = quad_sum(fma2(g, sp2(mmo), sp) + (r == 0 ? fma2(gs, sp2(mmo), sps) : f2{0.f, 0.f}));
-            if (r == 0 && idx < ncell && ((fl >> 25) & 1))
+            if (r == 0 && idx < ncell && ((fl >> 27) & 1))
                 L.part[((par * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] = part;
         }
         PSTAMP(5);
@@ -517,6 +530,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
     }
     const bool constrained = __syncthreads_or(cst);
+    PSTAMP(1);
     if (tid == 0) {   // ViennaRNA's S1 wrap-around
         L.S[0] = L.S[N];
         L.S[N + 1] = L.S[1];
@@ -541,7 +555,6 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const uint8_t *S = L.S;
     const float *ct = L.ct;
     const float sig1 = XS->sig[1], mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing;
-    const float eTAU = XS->ctab[CT_FSM + 6];
     const float mext = XS->motif_extra;
     const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
 
@@ -608,34 +621,51 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     __syncthreads();
     PSTAMP(0);
 
-    // ---- records (wave 13): the changed pairable cells of diagonal D (rank
+    // ---- records (wave 10): the changed pairable cells of diagonal D (rank
     // lists) and their setup values -- outer factors of the closing pair, the
     // unpaired runs, the 1x1..2x2 table factors (HBM/L2 loads) -- gathered at step
     // D - 2 (rec_load) and written at step D - 1 (rec_store), so the table loads
     // complete in the shadow of a step
     struct Pend {
         int n;                       // cells
-        int i[2], w1[2];             // per lane-set: i, ty | A << 8 | B << 16 | flags
-        float mmo[2], tau[2], mo[2], m23[2], t11[2], t12[2], t21[2], t22[2];
+        int w1[2];                   // per lane-set: the record word (pb_sweep)
+        float mmo[2], mo[2], m23[2], t11[2], t12[2], t21[2], t22[2];
     };
     struct Seq {                     // per lane-set: i and the bases around the closing pair
         int n;
         int i[2], sq[2];             // sq: ty | si1 << 4 | sj1 << 8 | si2 << 12 | sj2 << 16 | A << 20 (A, B: 6 bits)
         int ab[2];                   // A | B << 8
     };
-    // three stages a step apart: seq_load (rank list, bases), rec_load (tables:
-    // LDS factors, HBM/L2 1x1..2x2 factors), rec_store -- one LDS round trip each
-    auto seq_load = [&](int D) {
-        Seq Q;
-        Q.n = 0;
-        if (D < 6 || D > N - 1) return Q;
+    // four stages a step apart, one LDS round trip each: idx_load (rank list),
+    // seq_load (bases), rec_load (tables: LDS factors, HBM/L2 1x1..2x2
+    // factors), rec_store
+    struct Idx {                     // per lane-set: i of the lane's cell (the first cell on idle lanes)
+        int n;
+        int i[2];
+    };
+    auto idx_load = [&](int D) {
+        Idx X;
+        X.n = 0;
+        X.i[0] = X.i[1] = 1;
+        if (D < 6 || D > N - 1) return X;
         const int od = off(D, N);
-        Q.n = uni(L.cn[D]);
+        X.n = uni(L.cn[D]);
+        const int i0 = L.cl[od];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int idx = k * WAVE + lane;
+            const int ir = L.cl[od + min(idx, N - D - 1)];
+            X.i[k] = idx < X.n ? ir : i0;
+        }
+        return X;
+    };
+    auto seq_load = [&](int D, const Idx &X) {
+        Seq Q;
+        Q.n = X.n;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (k * WAVE >= Q.n) break;
-            const int idx = k * WAVE + lane;
-            const int i = L.cl[od + (idx < Q.n ? idx : 0)], j = i + D;
+            const int i = X.i[k], j = i + D;
             Q.i[k] = i;
             Q.sq[k] = ptype(S[i], S[j]) | (S[i + 1] << 4) | (S[j - 1] << 8) | (S[i + 2] << 12) | (S[j - 2] << 16);
             Q.ab[k] = L.up[i + 1] | (L.dn[j - 1] << 8);
@@ -666,10 +696,8 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 if (umax >= 4) P.t22[k] = T.int22[ty][t2of(2, 2)][si1][si2][sj2][sj1];
             }
             const bool mkc = A < umax || Bq < umax;
-            P.i[k] = i;
-            P.w1[k] = ty | (A << 8) | (Bq << 16) | (mkc ? (1 << 24) : 0) | (v ? (1 << 25) : 0);
+            P.w1[k] = i | (ty << 7) | (A << 10) | (Bq << 18) | (mkc ? (1 << 26) : 0) | (v ? (1 << 27) : 0);
             P.mmo[k] = L.dt[DT_MMI + oc];
-            P.tau[k] = ty > 2 ? eTAU : 1.f;
             P.mo[k] = ct[CT_ONEN + oc] * P.mmo[k];
             P.m23[k] = ct[CT_M23O + oc];
         }
@@ -680,25 +708,25 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         for (int k = 0; k < 2; k++) {
             if (k * WAVE >= P.n) break;
             float *r = L.rec + (((D & 1) * 2 + k) * PX_RF) * WAVE + lane;
-            r[0] = __int_as_float(P.i[k]);
-            r[WAVE] = __int_as_float(P.w1[k]);
-            r[2 * WAVE] = P.mmo[k];
-            r[3 * WAVE] = P.tau[k];
-            r[4 * WAVE] = P.mo[k];
-            r[5 * WAVE] = P.m23[k];
-            r[6 * WAVE] = P.t11[k];
-            r[7 * WAVE] = P.t12[k];
-            r[8 * WAVE] = P.t21[k];
-            r[9 * WAVE] = P.t22[k];
+            r[0] = __int_as_float(P.w1[k]);
+            r[WAVE] = P.mmo[k];
+            r[2 * WAVE] = P.mo[k];
+            r[3 * WAVE] = P.m23[k];
+            r[4 * WAVE] = P.t11[k];
+            r[5 * WAVE] = P.t12[k];
+            r[6 * WAVE] = P.t21[k];
+            r[7 * WAVE] = P.t22[k];
         }
         if (lane == 0) L.rcnt[D & 1] = P.n;
     };
     Pend pend;
     Seq seqp;
-    if (wid == PX_NW - 1) {
-        rec_store(4, rec_load(4, seq_load(4)));   // the sweep's first B diagonal (no loop fits: count 0)
-        pend = rec_load(5, seq_load(5));
-        seqp = seq_load(6);
+    Idx idxp;
+    if (wid == PX_WR) {
+        rec_store(4, rec_load(4, seq_load(4, idx_load(4))));   // the sweep's first B diagonal (no loop fits: count 0)
+        pend = rec_load(5, seq_load(5, idx_load(5)));
+        seqp = seq_load(6, idx_load(6));
+        idxp = idx_load(7);
     }
     __syncthreads();
 
@@ -720,19 +748,20 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             qf[h] = ok ? ct[CT_INVMM + L.cc[ix]] * e : 0.f;
         }
     };
-    if (wid == PX_NB + PX_NMW + 1) qfac(4);
+    if (wid == PX_WQ) qfac(4);
     const int s_end = N + 1;
     if (wid < PX_NB) {
         switch (wid) {
             // blocks of about equal LDS cost per lane-set (a size >= 6: 3 reads for
             // its special shapes + one per 4 generic ones; the small sizes ~3 per shape)
-            case 0: pb_sweep<30, 29, 0, 1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 1: pb_sweep<28, 27, 2, 6, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 2: pb_sweep<26, 25, 3, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            // (the heavier blocks on waves 2, 3, 6, 7: SIMDs 1 and 3 host one other role each)
+            case 0: pb_sweep<26, 25, 3, 8, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<28, 27, 2, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 2: pb_sweep<30, 29, 0, 1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 3: pb_sweep<24, 23, 4, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 4: pb_sweep<5, 7, 8, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 5: pb_sweep<22, 21, 20, 9, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 6: pb_sweep<19, 18, 17, 10, 11>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<18, 17, 10, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<20, 19, 9, 6, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<22, 21, 5, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             default: pb_sweep<16, 15, 14, 13, 12>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
     } else {
@@ -740,7 +769,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         // older (B) waves of the workgroup, so these run at a higher priority
         __builtin_amdgcn_s_setprio(2);
         for (int s = 4; s <= s_end; s++) {
-            if (wid < PX_NB + PX_NMW) {
+            if (px_mw(wid) >= 0) {
                 // ---------------- M: qm items of span sq = s - 2, K lanes per item (a
                 // power of two <= 16, one DPP row), split points in contiguous runs per
                 // lane, summed over the K lanes:
@@ -754,7 +783,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     int K = 16;
                     while (K > 1 && (N - sq) * K > PX_NMW * WAVE) K >>= 1;
                     const int ipw = WAVE / K;                 // items per wave
-                    const int mw = wid - PX_NB;
+                    const int mw = px_mw(wid);
                     const int k = lane & (K - 1);
                     const int item = mw * ipw + lane / K;
                     if (mw * ipw < n) {
@@ -798,7 +827,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         }
                     }
                 }
-            } else if (wid == PX_NB + PX_NMW) {
+            } else if (wid == PX_WF) {
                 // ---------------- F: the changed cells of diagonal e = s - 1
                 const int e = s - 1;
                 if (e >= 4 && e <= N - 1) {
@@ -831,7 +860,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         }
                     }
                 }
-            } else if (wid == PX_NB + PX_NMW + 1) {
+            } else if (wid == PX_WQ) {
                 // ---------------- Q: q5[j], j = s - 1 (column j is final); the
                 // exterior factors of column j + 1 are gathered one step ahead
                 const int j = s - 1;
@@ -849,12 +878,13 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sp2(sig1) : f2{0.f, 0.f}) + acc;
                 }
                 qfac(j + 1);
-            } else if (wid == PX_NW - 1) {
+            } else if (wid == PX_WR) {
                 // ---------------- R: records of diagonal s + 1 (next step's B), tables of
-                // s + 2, bases of s + 3
+                // s + 2, bases of s + 3, rank list of s + 4
                 rec_store(s + 1, pend);
                 pend = rec_load(s + 2, seqp);
-                seqp = seq_load(s + 3);
+                seqp = seq_load(s + 3, idxp);
+                idxp = idx_load(s + 4);
             }
             PSTAMP(4);
             lds_barrier();

@@ -29,8 +29,8 @@ L.adx_debug_stamps_pf(buf, 1)
 _, _, c = eng.download()
 scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = scored * max(1, eng.info.n_variants // 2)   # workgroups: one per (walker, apo/holo group)
-cols = ["setup", "-", "Bcell", "Bshape", "work", "Bwrite", "barrier"]
+cols = ["setup", "restore", "Bcell", "Bshape", "work", "Bwrite", "barrier"]
 print("cycles per workgroup per wave (N=%d, W=%d, %d steps, %.1f workgroups)" % (N, W, steps, G))
 print("wave " + " ".join("%9s" % n for n in cols))
-for w in range(14):
+for w in range(16):
     print("%4d " % w + " ".join("%9d" % (buf[w * 8 + k] // max(1, G)) for k in range(7)))
