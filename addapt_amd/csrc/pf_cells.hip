@@ -79,7 +79,7 @@ __device__ __forceinline__ f2 dpp_add2(f2 v) {
 
 struct PxLay {
     int C, NP;
-    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, Q5, CT, DT, PW, BY, BYTES;
+    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, Q5, CT, DT, PW, BY, MT, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit PxLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
@@ -98,6 +98,7 @@ struct PxLay {
         DT = o;   o += a16(size_t(DT_HP + N + 1) * 4);
         PW = o;   o += a16(size_t(N + 9) * 4);                    // (expMLbase sigma)^t
         BY = o;   o += a16(size_t(7) * NP);                       // S, up, dn, ptn, enc, flg, mat
+        MT = o;   o += a16(size_t(MAX_SPECIAL_HP) * 8 + 2 * MAX_MOTIF);   // special hairpins, motif codes / partners
         BYTES = o;
     }
 };
@@ -431,6 +432,10 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     L.enc = by + 4 * Y.NP;
     L.flg = by + 5 * Y.NP;
     L.mat = by + 6 * Y.NP;
+    uint32_t *spk = reinterpret_cast<uint32_t *>(smem + Y.MT);   // special-hairpin keys (padded: no match)
+    float *spv = reinterpret_cast<float *>(smem + Y.MT + MAX_SPECIAL_HP * 4);
+    uint8_t *mcode = reinterpret_cast<uint8_t *>(smem + Y.MT + MAX_SPECIAL_HP * 8);
+    int8_t *mpt = reinterpret_cast<int8_t *>(mcode + MAX_MOTIF);
     L.N = N;
     L.NP = Y.NP;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
@@ -465,6 +470,29 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
     auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
 
+    // ---- refold restore first: its HBM loads overlap the rest of the setup
+    if (incr) {
+        // refold: every table from the current slot (the changed cells are
+        // recomputed over it), two cells per lane and load, both folds interleaved
+        // (HBM side dword-aligned only when cells or B1 are odd: fine for global loads)
+        float4 *qd = reinterpret_cast<float4 *>(L.qb);   // qb, qm, q1 contiguous at a16(C + slack) strides
+        const int half = C >> 1;
+        const size_t ls4 = (Y.QM - Y.QB) >> 4;
+#pragma unroll 8   // N = 100: every load of a lane in flight at once
+        for (int k = tid; k < 3 * half; k += PX_NT) {
+            const int a = k / half, c = k - a * half;
+            const float *sa = src + a * Cs + 2 * c;
+            const float2 x = *reinterpret_cast<const float2 *>(sa), y = *reinterpret_cast<const float2 *>(sa + B1);
+            qd[a * ls4 + c] = float4{x.x, y.x, x.y, y.y};
+        }
+        if (C & 1)
+            for (int a = tid; a < 3; a += PX_NT) {
+                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
+            }
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
+    } else {
+        for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
+    }
     // ---- sequence, constraint arrays, tables (kernels.hip pf_group setup)
     const uint8_t *cons = ka.cons + V.cons_off;
     {
@@ -505,30 +533,17 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     for (int k = tid; k < 8; k += PX_NT) L.dt[DT_TAU + k] = T.termAU[k];
     for (int k = tid; k <= N; k += PX_NT) L.dt[DT_HP + k] = XS->hp[k];
     for (int k = tid; k < N + 9; k += PX_NT) L.pw[k] = XS->pwml[k];
+    for (int k = tid; k < MAX_SPECIAL_HP; k += PX_NT) {
+        const bool on = k < XS->n_special;
+        spk[k] = on ? XS->sp_key[k] : 0xFFFFFFFFu;   // hp_key never sets the top bits
+        spv[k] = on ? XS->sp_val[k] : 0.f;
+    }
+    for (int k = tid; k < MAX_MOTIF; k += PX_NT) {
+        mcode[k] = XS->motif_code[k];
+        mpt[k] = XS->motif_pt[k];
+    }
     for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
     for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
-    if (incr) {
-        // refold: every table from the current slot (the changed cells are
-        // recomputed over it), two cells per lane and load, both folds interleaved
-        // (HBM side dword-aligned only when cells or B1 are odd: fine for global loads)
-        float4 *qd = reinterpret_cast<float4 *>(L.qb);   // qb, qm, q1 contiguous at a16(C + slack) strides
-        const int half = C >> 1;
-        const size_t ls4 = (Y.QM - Y.QB) >> 4;
-#pragma unroll 4
-        for (int k = tid; k < 3 * half; k += PX_NT) {
-            const int a = k / half, c = k - a * half;
-            const float *sa = src + a * Cs + 2 * c;
-            const float2 x = *reinterpret_cast<const float2 *>(sa), y = *reinterpret_cast<const float2 *>(sa + B1);
-            qd[a * ls4 + c] = float4{x.x, y.x, x.y, y.y};
-        }
-        if (C & 1)
-            for (int a = tid; a < 3; a += PX_NT) {
-                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
-            }
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
-    } else {
-        for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
-    }
     const bool constrained = __syncthreads_or(cst);
     PSTAMP(1);
     if (tid == 0) {   // ViennaRNA's S1 wrap-around
@@ -539,16 +554,24 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const bool any_motif = (hol0 || hol1) && mL > 0;
     __syncthreads();
     if (any_motif) {
+        // motif sites: the sequence (one lane per start), then the constraints of
+        // each matching start (one wave per start, lanes = motif positions)
         for (int o = tid + 1; o + mL - 1 <= N; o += PX_NT) {
             bool ok = true;
-            for (int k = 0; k < mL && ok; k++)
-                if (L.S[o + k] != XS->motif_code[k]) ok = false;
-            for (int k = 0; k < mL && ok; k++) {
-                const int pk = XS->motif_pt[k];
-                if (pk < 0) ok = L.up[o + k] >= 1;
-                else if (pk > k) ok = px_allowed(L, o + k, o + pk);
-            }
+            for (int k = 0; k < mL && ok; k++) ok = L.S[o + k] == mcode[k];
             L.mat[o] = ok ? 1 : 0;
+        }
+        __syncthreads();
+        for (int o = 1 + wid; o + mL - 1 <= N; o += PX_NW) {
+            if (!uni(L.mat[o])) continue;
+            bool ok = true;
+            for (int k = lane; k < mL; k += WAVE) {
+                const int pk = mpt[k];
+                if (pk < 0) ok = ok && L.up[o + k] >= 1;
+                else if (pk > k) ok = ok && px_allowed(L, o + k, o + pk);
+            }
+            const bool all = __ballot(!ok) == 0;
+            if (lane == 0) L.mat[o] = all ? 1 : 0;
         }
     }
     __syncthreads();
@@ -579,8 +602,11 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     bool special = false;
                     if (u == 3 || u == 4 || u == 6) {
                         const uint32_t key = hp_key(S, i, u + 2);
-                        for (int q = 0; q < nsp; q++)
-                            if (XS->sp_key[q] == key) { h = XS->sp_val[q]; special = true; break; }
+                        for (int q0 = 0; q0 < nsp; q0 += 8) {   // 8 independent LDS reads per round
+#pragma unroll
+                            for (int t = 0; t < 8; t++)
+                                if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
+                        }
                     }
                     if (!special)
                         h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type] : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
