@@ -584,65 +584,65 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     // cells by diagonal (wave w: diagonals 4 + w, 4 + w + NW, ...; lanes = i): the
     // inner code of every cell; the changed cells' hairpin (+ motif) initial value
     // (pairable) or the mark, and multiloop stem in qm1 (F reads both before it
-    // overwrites them); in a refold every other cell was restored above
-    for (int D = 4 + wid; D <= N - 1; D += PX_NW) {
-        const int od = off(D, N), lo = clo(D), hi = chi(D);
-        for (int i = 1 + lane; i <= N - D; i += WAVE) {
-            const int j = i + D;
-            const int type = ptype(S[i], S[j]);
-            L.cc[od + i - 1] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
-            if (i < lo || i > hi) continue;
-            const bool pr = type != 0 && px_allowed(L, i, j);
-            f2 init = f2{-0.f, -0.f};
-            float m1 = 0.f;
-            if (pr) {
-                const int u = D - 1;
-                float h = 0.f;
-                if (L.up[i + 1] >= u) {
-                    bool special = false;
-                    if (u == 3 || u == 4 || u == 6) {
-                        const uint32_t key = hp_key(S, i, u + 2);
-                        for (int q0 = 0; q0 < nsp; q0 += 8) {   // 8 independent LDS reads per round
-#pragma unroll
-                            for (int t = 0; t < 8; t++)
-                                if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
-                        }
-                    }
-                    if (!special)
-                        h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type] : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
-                }
-                const bool mx = D == mL - 1 && mL > 0 && L.mat[i];
-                init = f2{(mx && hol0) ? h + mext : h, (mx && hol1) ? h + mext : h};
-                m1 = L.dt[DT_MLS + type * 25 + S[i - 1] * 5 + S[j + 1]];
-            }
-            L.qb[od + i - 1] = init;
-            L.q1[colb(j) + i - 1] = f2{m1, m1};
-        }
-    }
-    for (int k = tid; k <= 3 && k <= N; k += PX_NT) {   // q5[0..3] (pf_group: unpaired prefix)
-            float q = 1.f;
-            bool ok = true;
-            for (int t = 1; t <= k; t++) {
-                ok = ok && L.up[t] >= 1;
-                q *= sig1;
-            }
-            L.q5[k] = ok ? f2{q, q} : f2{0.f, 0.f};
-    }
-    __syncthreads();
-    // rank lists of the changed pairable cells per diagonal (the B lanes; the mark
-    // is final after the pass above): cl[off(D) + rank] = i, cn[D] = count
+    // overwrites them) -- in a refold every other cell was restored above; and the
+    // rank list of the changed pairable cells (the B lanes): cl[off(D) + rank] = i,
+    // cn[D] = count
     for (int D = 4 + wid; D <= N - 1; D += PX_NW) {
         const int od = off(D, N), lo = clo(D), hi = chi(D);
         int base = 0;
-        for (int i0 = lo; i0 <= hi; i0 += WAVE) {
+        for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
             const int i = i0 + lane;
-            const bool pr = i <= hi && !is_mark2(L.qb[od + i - 1]);
+            const bool cell = i <= N - D;
+            const bool inb = cell && i >= lo && i <= hi;
+            bool pr = false;
+            if (cell) {
+                const int j = i + D;
+                const int type = ptype(S[i], S[j]);
+                L.cc[od + i - 1] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
+                if (inb) {
+                    pr = type != 0 && px_allowed(L, i, j);
+                    f2 init = f2{-0.f, -0.f};
+                    float m1 = 0.f;
+                    if (pr) {
+                        const int u = D - 1;
+                        float h = 0.f;
+                        if (L.up[i + 1] >= u) {
+                            bool special = false;
+                            if (u == 3 || u == 4 || u == 6) {
+                                const uint32_t key = hp_key(S, i, u + 2);
+                                for (int q0 = 0; q0 < nsp; q0 += 8) {   // 8 independent LDS reads per round
+#pragma unroll
+                                    for (int t = 0; t < 8; t++)
+                                        if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
+                                }
+                            }
+                            if (!special)
+                                h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type]
+                                                                : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
+                        }
+                        const bool mx = D == mL - 1 && mL > 0 && L.mat[i];
+                        init = f2{(mx && hol0) ? h + mext : h, (mx && hol1) ? h + mext : h};
+                        m1 = L.dt[DT_MLS + type * 25 + S[i - 1] * 5 + S[j + 1]];
+                    }
+                    L.qb[od + i - 1] = init;
+                    L.q1[colb(j) + i - 1] = f2{m1, m1};
+                }
+            }
             const uint64_t m = __ballot(pr);
             const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
             if (pr) L.cl[od + slot] = uint8_t(i);
             base += __popcll(m);
         }
         if (lane == 0) L.cn[D] = uint8_t(base);
+    }
+    for (int k = tid; k <= 3 && k <= N; k += PX_NT) {   // q5[0..3] (pf_group: unpaired prefix)
+        float q = 1.f;
+        bool ok = true;
+        for (int t = 1; t <= k; t++) {
+            ok = ok && L.up[t] >= 1;
+            q *= sig1;
+        }
+        L.q5[k] = ok ? f2{q, q} : f2{0.f, 0.f};
     }
     __syncthreads();
     PSTAMP(0);
