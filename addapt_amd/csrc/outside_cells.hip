@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 
 #include "dev_types.hpp"
@@ -206,6 +207,66 @@ struct OxSize {
     }
 };
 
+// Loop size U >= 6 over the four lanes of an inner cell (phase r = lane & 3),
+// as pf_cells.hip PxSizeQ: lane r takes one special shape -- the bulges (0,U)
+// (U,0) and 1 x n loops (1,U-1) (U-1,1), a window read, an outer-code read and
+// a factor gather -- and the generic shapes n1 = 2 + r + 4m <= U - 2 (one
+// window read at a per-lane base + immediate offset, its factor in a VGPR; 0
+// past the size).  The four lanes' sums are added in a fixed order.
+template <int U>
+struct OxSizeQ {
+    static constexpr int NR = U >= 6 ? (U - 3 + 3) / 4 : 1;
+    float gf[NR];
+    float fsp;
+    int n1sp;
+    __device__ __forceinline__ void load(const OxL &L, int r) {
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const int n1 = 2 + 4 * m + r;
+            gf[m] = n1 <= U - 2 ? L.sf[U * 32 + n1] : 0.f;
+        }
+        n1sp = r == 0 ? 0 : r == 1 ? U : r == 2 ? 1 : U - 1;
+        fsp = L.sf[U * 32 + n1sp];
+    }
+    __device__ __forceinline__ void run(const OxL &L, const OxCell &c, int d, int umax, int ctb, float outer,
+                                        float &g, float &sp) const {
+        if (U <= umax) {
+            const int o = wslot(d + 2 + U) * L.RL + OX_PAD + c.i - 2 - U;   // shape n1 at o + U - n1
+            {
+                const float v = L.qw[o + U - n1sp];
+                const int oc = L.ow[o + U - n1sp];
+                sp = fmaf(v, L.ct[ctb + oc] * (outer * fsp), sp);
+            }
+            const float *q = L.qw + o + U - 2 - (threadIdx.x & 3);
+#pragma unroll
+            for (int m = 0; m < NR; m++) g = fmaf(q[-4 * m], gf[m], g);
+        }
+    }
+};
+template <int U>
+struct OxBlk {   // the size's state in a B wave (sizes <= 5 whole in every lane)
+    using T = typename std::conditional<(U <= 5), OxSize<U>, OxSizeQ<U>>::type;
+};
+template <int U>
+__device__ __forceinline__ void ox_load(typename OxBlk<U>::T &z, const OxL &L, int r) {
+    if constexpr (U <= 5) z.load(L);
+    else z.load(L, r);
+}
+template <int U>
+__device__ __forceinline__ void ox_run(const typename OxBlk<U>::T &z, const OxL &L, const OxCell &c, int d, int umax,
+                                       int ty2, int ctb, float outer, float &g, float &sp, float &gs, float &sps) {
+    if constexpr (U < 0) {
+    } else if constexpr (U <= 5) {
+        z.run(L, c, d, umax, ty2, gs, sps);
+    } else {
+        z.run(L, c, d, umax, ctb, outer, g, sp);
+    }
+}
+__device__ __forceinline__ float quad_sum_f(float v) {   // sum over the 4 lanes of a quad, in every lane
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));   // [1,0,3,2]
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));   // [2,3,0,1]
+}
+
 #ifdef ADX_STAMP
 #define OX_STP_PARAMS , unsigned long long *st_acc, unsigned long long &st_last
 #define OX_STP_ARGS , st_acc, st_last
@@ -215,51 +276,62 @@ struct OxSize {
 #endif
 
 // B: the interior-loop gather of every diagonal for one block of loop sizes
-// (U3..U0, -1 = none), the block's shape factors held in registers for the
-// whole sweep; one barrier per diagonal, as the M / F waves.
-template <int U0, int U1, int U2, int U3, class Fin>
+// (-1 = none), the block's shape factors held in registers for the whole sweep;
+// four lanes per inner cell (16 cells per lane-set; OxSizeQ), one barrier per
+// diagonal, as the M / F waves.
+template <int U0, int U1, int U2, int U3, int U4, class Fin>
 __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, const Fin &fin OX_STP_PARAMS) {
-    constexpr bool TB = (U0 >= 2 && U0 <= 4) || (U1 >= 2 && U1 <= 4) || (U2 >= 2 && U2 <= 4) || (U3 >= 2 && U3 <= 4);
-    OxSize<U0> s0;
-    OxSize<U1> s1;
-    OxSize<U2> s2;
-    OxSize<U3> s3;
-    s0.load(L);
-    s1.load(L);
-    s2.load(L);
-    s3.load(L);
+    constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
+    constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
+    const int r = lane & 3, cq = lane >> 2;
+    typename OxBlk<U0>::T s0;
+    typename OxBlk<U1>::T s1;
+    typename OxBlk<U2>::T s2;
+    typename OxBlk<U3>::T s3;
+    typename OxBlk<U4>::T s4;
+    ox_load<U0>(s0, L, r);
+    ox_load<U1>(s1, L, r);
+    ox_load<U2>(s2, L, r);
+    ox_load<U3>(s3, L, r);
+    ox_load<U4>(s4, L, r);
+    const int ctb = r < 2 ? CT_BUL : CT_ONEN;   // the lane's special-shape outer factor table
     for (int d = N - 1; d >= 3; d--) {
         const int par = d & 1;
         const int umax = min(30, N - 3 - d);                      // outer spans d+2 .. d+2+umax
         // lanes = the pairable cells of diagonal d, compacted (records one step ahead)
-        const int ncls = (d >= 4 && umax >= 0) ? (uni(L.rcnt[par]) + WAVE - 1) / WAVE : 0;
-        for (int ls = 0; ls < ncls; ls++) {
-            const float *r = L.rec + ((par * 2 + ls) * OX_RF) * WAVE + lane;
-            const int tp = __float_as_int(r[8 * WAVE]);
-            const int i = __float_as_int(r[9 * WAVE]);
+        const int ncell = (d >= 4 && umax >= 0) ? uni(L.rcnt[par]) : 0;
+        for (int c0 = 0; c0 < ncell; c0 += WAVE / 4) {
+            const int idx = c0 + cq;   // the lane's cell (records: set idx / 64, lane idx % 64)
+            const float *rr = L.rec + ((par * 2 + (idx >> 6)) * OX_RF) * WAVE + (idx & (WAVE - 1));
+            const int tp = __float_as_int(rr[8 * WAVE]);
+            const int i = __float_as_int(rr[9 * WAVE]);
             OxCell c;
             c.i = i;
             const int ty2 = tp & 255;
-            c.mmin = r[0];
-            c.tau_in = r[WAVE];
-            c.mo_in = r[2 * WAVE];
-            c.m23_in = r[3 * WAVE];
+            c.mmin = rr[0];
+            c.tau_in = rr[WAVE];
+            c.mo_in = rr[2 * WAVE];
+            c.m23_in = rr[3 * WAVE];
             c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
             if constexpr (TB) {
-                c.t11 = r[4 * WAVE];
-                c.t12 = r[5 * WAVE];
-                c.t21 = r[6 * WAVE];
-                c.t22 = r[7 * WAVE];
+                c.t11 = rr[4 * WAVE];
+                c.t12 = rr[5 * WAVE];
+                c.t21 = rr[6 * WAVE];
+                c.t22 = rr[7 * WAVE];
             }
-            float g = 0.f, sp = 0.f;
+            const float outer = r < 2 ? c.tau_in : c.mo_in;
+            float g = 0.f, sp = 0.f, gs = 0.f, sps = 0.f;
             OSTAMP(2);   // B cell setup
-            s0.run(L, c, d, umax, ty2, g, sp);
-            s1.run(L, c, d, umax, ty2, g, sp);
-            s2.run(L, c, d, umax, ty2, g, sp);
-            s3.run(L, c, d, umax, ty2, g, sp);
+            ox_run<U0>(s0, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
+            ox_run<U1>(s1, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
+            ox_run<U2>(s2, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
+            ox_run<U3>(s3, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
+            ox_run<U4>(s4, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
             OSTAMP(3);   // B shapes
-            if (tp >= 256)   // the cell's natural slot (F reads lane = cell)
-                L.part[((par * 2 + ((i - 1) >> 6)) * OX_NB + wid) * WAVE + ((i - 1) & (WAVE - 1))] = fmaf(g, c.mmin, sp);
+            // small sizes count once (phase 0), then the cell's total over its four lanes
+            const float part = quad_sum_f(fmaf(g, c.mmin, sp) + (r == 0 ? fmaf(gs, c.mmin, sps) : 0.f));
+            if (r == 0 && idx < ncell && tp >= 256)   // the cell's natural slot (F reads lane = cell)
+                L.part[((par * 2 + ((i - 1) >> 6)) * OX_NB + wid) * WAVE + ((i - 1) & (WAVE - 1))] = part;
         }
         fin(d);   // F of diagonal d + 1 on waves 0 and 1
         OSTAMP(5);
@@ -675,16 +747,20 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     // a special ~9); the 1x1..2x2 table shapes (u = 2, 3, 4) last in their blocks
     if (wid < OX_NB) {
         switch (wid) {
-            case 0: b_sweep<30, 12, 1, 0>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 1: b_sweep<29, 11, 5, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 2: b_sweep<28, 13, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 3: b_sweep<27, 14, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 4: b_sweep<26, 15, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 5: b_sweep<25, 16, 4, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 6: b_sweep<24, 17, 7, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 7: b_sweep<23, 18, 6, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 8: b_sweep<22, 19, 3, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            default: b_sweep<21, 20, 2, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            // loop sizes spread so that every wave's B blocks plus its other role take
+            // about the same time (stamps, tools/outside_stamps.py): the finalize
+            // wave 0 one size and the record wave 7 none (a size >= 6 costs 3 reads for its
+            // special shapes + one per 4 generic ones per lane-set, sizes <= 5 ~3 per shape)
+            case 0: b_sweep<19, -1, -1, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 1: b_sweep<5, 7, 15, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 2: b_sweep<4, 0, 23, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 3: b_sweep<3, 30, 6, 11, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 4: b_sweep<29, 28, 27, 1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 5: b_sweep<26, 25, 24, 2, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 6: b_sweep<22, 21, 20, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 7: b_sweep<-1, -1, -1, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 8: b_sweep<18, 17, 16, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            default: b_sweep<14, 13, 12, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
         }
     } else for (int d = N - 1; d >= 3; d--) {
         const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
