@@ -84,7 +84,7 @@ struct OxLay {
         PART = o; o += a16(size_t(2) * 2 * OX_NB * WAVE * 4);   // [parity][lane-set][block][lane]
         MLP = o;  o += a16(size_t(2) * OX_NM * WAVE * 4);       // [parity][M wave][lane]
         REC = o;  o += a16(size_t(2) * 2 * OX_RF * WAVE * 4 + 16);   // cell setup records [parity][lane-set][field][lane]; counts [parity]
-        CL = o;   o += a16(size_t(2) * 2 * WAVE);                // compacted pairable cells [parity][slot]
+        CL = o;   o += a16(size_t(C) + size_t(NP));              // pairable cells per diagonal: cl[off(D) + rank] = i; counts
         FR = o;   o += a16(size_t(2) * 2 * OX_FF * WAVE * 4);   // finalize records [parity][lane-set][field][lane]
         SF = o;   o += a16(size_t(31) * 32 * 4);                 // constant factor of shape (u, n1): [u][n1]
         RQ = o;   o += a16(size_t(2) * NP * 4);                  // qmb ring [parity][i]
@@ -371,6 +371,7 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     L.rec = reinterpret_cast<float *>(smem + Y.REC);
     L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(2) * 2 * OX_RF * WAVE * 4);
     L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);
+    uint8_t *cn = L.cl + Y.C;   // cn[D]: pairable cells of diagonal D
     L.sf = reinterpret_cast<float *>(smem + Y.SF);
     L.fr = reinterpret_cast<float *>(smem + Y.FR);
     L.rq = reinterpret_cast<float *>(smem + Y.RQ);
@@ -559,6 +560,21 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         L.ow[k] = 0;
     }
     for (int k = tid; k < C; k += OX_NT) L.yc[k] = 0.f;
+    // the pairable cells of every diagonal in rank order (the B lanes; an
+    // unconstrained fold: the pair type alone decides)
+    for (int D = 4 + wid; D <= N - 1; D += OX_NW) {
+        const int od = off(D, N);
+        int base = 0;
+        for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
+            const int i = i0 + lane;
+            const bool pr = i <= N - D && ptype(S[i], S[i + D]) != 0;
+            const uint64_t m = __ballot(pr);
+            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            if (pr) L.cl[od + slot] = uint8_t(i);
+            base += __popcll(m);
+        }
+        if (lane == 0) cn[D] = uint8_t(base);
+    }
     __syncthreads();
 
     OSTAMP(1);   // exterior adjoint + zeroing
@@ -576,43 +592,54 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         j = i + D;
         return valid;
     };
-    // The pairable cells of diagonal D are compacted (ballot + mbcnt over the
-    // natural lane-sets, one wave): compacted lane-set k holds cells
-    // ci[k] (0: none), whose table factors t[k] are loaded one step before the
-    // record is written.
-    struct Pend {
-        int ci[2];
-        float4 t[2];
+    // The records of diagonal D's pairable cells (rank lists built in setup) in
+    // three stages a step apart, one LDS round trip each: idx_load (rank list),
+    // tab_load (bases, the cell's LDS factors, the 1x1..2x2 table factors from
+    // HBM/L2), rec_write (stores only).
+    struct Idx {
         int cnt;
+        int i[2];   // the lane's cell (cell 1 on idle lanes: its shapes are read and discarded)
     };
-    auto tab_load = [&](int D) {
-        Pend P;
-        P.ci[0] = P.ci[1] = 0;
-        P.t[0] = P.t[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        P.cnt = 0;
-        if (D < 4) return P;
-        const int umax = min(30, N - 3 - D);
-        const int nls = (N - D + WAVE - 1) / WAVE;
-        int base = 0;
-        for (int ls = 0; ls < nls; ls++) {
-            const int i = 1 + ls * WAVE + lane;
-            const bool pr = i <= N - D && ptype(S[i], S[i + D]) != 0;
-            const uint64_t m = __ballot(pr);
-            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-            if (pr) L.cl[(D & 1) * 2 * WAVE + slot] = uint8_t(i);
-            base += __popcll(m);
-        }
-        P.cnt = base;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
+    auto idx_load = [&](int D) {
+        Idx X;
+        X.cnt = 0;
+        X.i[0] = X.i[1] = 1;
+        if (D < 4) return X;
+        const int od = off(D, N);
+        X.cnt = uni(cn[D]);
+#pragma unroll
         for (int k = 0; k < 2; k++) {
             const int idx = k * WAVE + lane;
-            if (idx >= base) continue;
-            const int i = L.cl[(D & 1) * 2 * WAVE + idx], j = i + D;
-            P.ci[k] = i;
+            const int ir = L.cl[od + min(idx, N - D - 1)];
+            X.i[k] = idx < X.cnt ? ir : 1;
+        }
+        return X;
+    };
+    struct Pend {
+        int cnt;
+        int i[2], ty2[2];
+        float mmin[2], mo[2], m23[2];
+        float4 t[2];
+    };
+    auto tab_load = [&](int D, const Idx &X) {
+        Pend P;
+        P.cnt = X.cnt;
+        const int umax = min(30, N - 3 - D);
+        auto Sc = [&](int x) { return int(S[x < 0 ? 0 : (x > N + 1 ? N + 1 : x)]); };
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            P.i[k] = X.i[k];
+            P.ty2[k] = 0;
+            P.mmin[k] = P.mo[k] = P.m23[k] = 0.f;
+            P.t[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k * WAVE >= X.cnt) continue;
+            const int i = X.i[k], j = i + D;
             const int ty2 = rtype(ptype(S[i], S[j]));
+            const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
+            P.ty2[k] = ty2;
+            P.mmin[k] = L.dt[DT_MMI + cc];
+            P.mo[k] = ct[CT_ONEN + cc] * P.mmin[k];
+            P.m23[k] = ct[CT_M23O + cc];
             float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
             if (umax >= 2) t.x = T.int11[ptype(Sc(i - 2), Sc(j + 2))][ty2][Sc(i - 1)][Sc(j + 1)];
             if (umax >= 3) {
@@ -632,30 +659,28 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             const int idx = k * WAVE + lane;
             if (k * WAVE >= P.cnt) break;
             const bool v = idx < P.cnt;
-            const int i = v ? P.ci[k] : 1, j = i + D;
-            const int ty2 = rtype(ptype(S[i], S[j]));
-            const int cc = ty2 * 25 + S[j + 1] * 5 + S[i - 1];
-            const float mmin = L.dt[DT_MMI + cc];
             float *r = L.rec + (((D & 1) * 2 + k) * OX_RF) * WAVE + lane;
-            r[0 * WAVE] = mmin;
-            r[1 * WAVE] = ty2 > 2 ? eTAU : 1.f;
-            r[2 * WAVE] = ct[CT_ONEN + cc] * mmin;
-            r[3 * WAVE] = ct[CT_M23O + cc];
+            r[0 * WAVE] = P.mmin[k];
+            r[1 * WAVE] = P.ty2[k] > 2 ? eTAU : 1.f;
+            r[2 * WAVE] = P.mo[k];
+            r[3 * WAVE] = P.m23[k];
             r[4 * WAVE] = P.t[k].x;
             r[5 * WAVE] = P.t[k].y;
             r[6 * WAVE] = P.t[k].z;
             r[7 * WAVE] = P.t[k].w;
-            r[8 * WAVE] = __int_as_float(ty2 | (v ? 256 : 0));
-            r[9 * WAVE] = __int_as_float(i);   // an idle lane reads cell 1's shapes (discarded)
+            r[8 * WAVE] = __int_as_float(P.ty2[k] | (v ? 256 : 0));
+            r[9 * WAVE] = __int_as_float(P.i[k]);   // an idle lane reads cell 1's shapes (discarded)
         }
     };
     constexpr int RW = 7;   // B wave RW: setup records (both lane-sets)
-    Pend pnext;             // compaction + table factors of the diagonal after the next
-    pnext.ci[0] = pnext.ci[1] = 0;
+    Pend pnext;             // the factors of the diagonal after the next
+    Idx inext;              // the rank list of the one after that
     pnext.cnt = 0;
+    inext.cnt = 0;
     if (wid == RW) {
-        rec_write(N - 1, tab_load(N - 1));
-        pnext = tab_load(N - 2);
+        rec_write(N - 1, tab_load(N - 1, idx_load(N - 1)));
+        pnext = tab_load(N - 2, idx_load(N - 2));
+        inext = idx_load(N - 3);
     }
     __syncthreads();
 
@@ -735,10 +760,11 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         } else if (wid < 4) {
             frec_write(d, wid - 2);   // diagonal d, finalized next step
         } else if (wid == RW) {
-            // setup records of diagonal d - 1 (next step's B), with the compaction and
-            // table factors made last step; those of diagonal d - 2
+            // setup records of diagonal d - 1 (next step's B) from the factors made last
+            // step; the factors of diagonal d - 2, the rank list of d - 3
             rec_write(d - 1, pnext);
-            pnext = tab_load(d - 2);
+            pnext = tab_load(d - 2, inext);
+            inext = idx_load(d - 3);
         }
     };
 
