@@ -62,7 +62,7 @@ constexpr int OX_MAXP = 64;           // requested pairs of one fold kept in LDS
 constexpr int OX_NMAX = 112;
 constexpr int OX_SLACK = 64;          // zeroed floats after each cell table (reads past a row end)
 constexpr int OX_FF = 5;              // finalize record fields (see frec_write)
-constexpr int OX_RF = 10;             // cell setup record fields (see rec_write)
+constexpr int OX_RF = 8;              // cell setup record fields (see rec_write)
 
 // LDS carve for folded length N (runtime; the host sizes the launch with it)
 struct OxLay {
@@ -283,6 +283,7 @@ template <int U0, int U1, int U2, int U3, int U4, class Fin>
 __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, const Fin &fin OX_STP_PARAMS) {
     constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
     constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
+    constexpr bool H5 = U0 == 5 || U1 == 5 || U2 == 5 || U3 == 5 || U4 == 5;   // 2x3 loops (m23)
     const int r = lane & 3, cq = lane >> 2;
     typename OxBlk<U0>::T s0;
     typename OxBlk<U1>::T s1;
@@ -295,6 +296,7 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
     ox_load<U3>(s3, L, r);
     ox_load<U4>(s4, L, r);
     const int ctb = r < 2 ? CT_BUL : CT_ONEN;   // the lane's special-shape outer factor table
+    const float eTAU = L.ct[CT_FSM + 6];
     for (int d = N - 1; d >= 3; d--) {
         const int par = d & 1;
         const int umax = min(30, N - 3 - d);                      // outer spans d+2 .. d+2+umax
@@ -303,15 +305,16 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
         for (int c0 = 0; c0 < ncell; c0 += WAVE / 4) {
             const int idx = c0 + cq;   // the lane's cell (records: set idx / 64, lane idx % 64)
             const float *rr = L.rec + ((par * 2 + (idx >> 6)) * OX_RF) * WAVE + (idx & (WAVE - 1));
-            const int tp = __float_as_int(rr[8 * WAVE]);
-            const int i = __float_as_int(rr[9 * WAVE]);
+            // word: i | ty2 << 8 | real << 16; a block reads only the fields its sizes use
+            const int tp = __float_as_int(rr[0]);
+            const int i = tp & 255;
             OxCell c;
             c.i = i;
-            const int ty2 = tp & 255;
-            c.mmin = rr[0];
-            c.tau_in = rr[WAVE];
+            const int ty2 = (tp >> 8) & 255;
+            c.mmin = rr[WAVE];
+            c.tau_in = ty2 > 2 ? eTAU : 1.f;
             c.mo_in = rr[2 * WAVE];
-            c.m23_in = rr[3 * WAVE];
+            c.m23_in = H5 ? rr[3 * WAVE] : 0.f;
             c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
             if constexpr (TB) {
                 c.t11 = rr[4 * WAVE];
@@ -330,7 +333,7 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
             OSTAMP(3);   // B shapes
             // small sizes count once (phase 0), then the cell's total over its four lanes
             const float part = quad_sum_f(fmaf(g, c.mmin, sp) + (r == 0 ? fmaf(gs, c.mmin, sps) : 0.f));
-            if (r == 0 && idx < ncell && tp >= 256)   // the cell's natural slot (F reads lane = cell)
+            if (r == 0 && idx < ncell && (tp >> 16))   // the cell's natural slot (F reads lane = cell)
                 L.part[((par * 2 + ((i - 1) >> 6)) * OX_NB + wid) * WAVE + ((i - 1) & (WAVE - 1))] = part;
         }
         fin(d);   // F of diagonal d + 1 on waves 0 and 1
@@ -579,7 +582,6 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
 
     OSTAMP(1);   // exterior adjoint + zeroing
     const float mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing, pw1 = XS->pwml[1];
-    const float eTAU = XS->ctab[CT_FSM + 6];
 
     // Setup record of the cells of lane-set ls of diagonal D, written one step
     // before B reads it: inner mismatch, TermAU, 1xn / 2x3 factors of the cell as
@@ -660,16 +662,15 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             if (k * WAVE >= P.cnt) break;
             const bool v = idx < P.cnt;
             float *r = L.rec + (((D & 1) * 2 + k) * OX_RF) * WAVE + lane;
-            r[0 * WAVE] = P.mmin[k];
-            r[1 * WAVE] = P.ty2[k] > 2 ? eTAU : 1.f;
+            // an idle lane reads cell 1's shapes (discarded)
+            r[0 * WAVE] = __int_as_float(P.i[k] | (P.ty2[k] << 8) | (v ? (1 << 16) : 0));
+            r[1 * WAVE] = P.mmin[k];
             r[2 * WAVE] = P.mo[k];
             r[3 * WAVE] = P.m23[k];
             r[4 * WAVE] = P.t[k].x;
             r[5 * WAVE] = P.t[k].y;
             r[6 * WAVE] = P.t[k].z;
             r[7 * WAVE] = P.t[k].w;
-            r[8 * WAVE] = __int_as_float(P.ty2[k] | (v ? 256 : 0));
-            r[9 * WAVE] = __int_as_float(P.i[k]);   // an idle lane reads cell 1's shapes (discarded)
         }
     };
     constexpr int RW = 7;   // B wave RW: setup records (both lane-sets)

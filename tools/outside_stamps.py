@@ -26,7 +26,7 @@ L.adx_debug_stamps_outside(buf, 1)
 eng.run_steps(steps)
 L.adx_debug_stamps_outside(buf, 1)
 _, _, c = eng.download()
-scored = int(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) * steps / max(1, c.sum())
+scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = 2 * scored   # outside folds (apo, holo) of the scored walkers
 cols = ["setup", "q5b", "Bcell", "Bshape", "M", "F/tail", "barrier"]
 print("cycles per outside fold per wave (N=%d, W=%d, %d steps, %.1f folds)" % (N, W, steps, G))
