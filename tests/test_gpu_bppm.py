@@ -144,11 +144,12 @@ def test_mc_trajectory_with_pair_terms(native, oracle):
         assert list(counters[w]) == ref["counters"]
 
 
-@pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (150, False)])
+@pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (110, False), (150, False)])
 def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
-    """Configs 3 / 4 shape: inside folds first, the outside pass on the
-    proposal's stored inside tables (N <= 128: outside_cells_kernel, lanes =
-    cells; N = 150: bppm_kernel with global scratch), then the scores.  Every
+    """Configs 3 / 4 shape: inside folds first (N <= 100: pf_cells_kernel,
+    else score_kernel), the outside pass on the proposal's stored inside tables
+    (N <= 112: outside_cells_kernel, lanes = cells; N = 150: bppm_kernel with
+    global scratch), then the scores.  Every
     scored proposal's score matches the oracle's from-scratch score of that
     proposal (ln p terms within 2e-3).  motif_pairs: pair terms inside the
     ligand motif (credited from the motif's closing cell in the holo fold)."""
