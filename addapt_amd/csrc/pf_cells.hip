@@ -8,17 +8,17 @@
 //     variants of one (context, macrostate)), the two folds in lockstep as
 //     float2 (ds_read_b64, v_pk_fma_f32: one instruction serves both);
 //   * one anti-diagonal per step, ONE barrier per step.  Step s runs
-//       B   the interior-loop sums of diagonal s (waves 0-7, loop sizes in
+//       B   the interior-loop sums of diagonal s (waves 0-6, loop sizes in
 //           blocks of equal cost; four lanes per changed pairable cell, each
 //           taking a quarter of a size's shapes; every shape one read of the
 //           inner cell at a per-lane base plus an immediate offset);
-//       M   the qm (fML) items of span s-2 (waves 11-13; K lanes per item so
+//       M   the qm (fML) items of span s-2 (waves 10-13; K lanes per item so
 //           that the few long items of late spans spread over the waves, the
 //           split points read from the row-major qm and column-major qm1 at
 //           immediate offsets);
-//       F   the cells of diagonal s-1 (wave 8): qb, qbm, qm1;
-//       Q   q5[s-1] (wave 9);
-//       R   the setup records of diagonal s+1 (wave 10), built in four
+//       F   the cells of diagonal s-1 (wave 7): qb, qbm, qm1;
+//       Q   q5[s-1] (wave 8);
+//       R   the setup records of diagonal s+1 (wave 9), built in four
 //           stages a step apart.
 //
 // Covered: N <= 100 (LDS); longer folds take kernels.hip score_kernel.
@@ -38,15 +38,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int PX_NW = 14;
 constexpr int PX_NT = PX_NW * WAVE;
-constexpr int PX_NB = 8;              // interior-loop blocks (waves 0..7)
-constexpr int PX_NMW = 3;             // qm item waves
-// Roles of waves 8-13.  A workgroup's waves go to SIMDs 0, 2, 1, 3, 0, 2, ...
-// (wave w on SIMD {0,2,1,3}[w % 4]), so SIMDs 0 and 2 host two of these waves
-// and 1 and 3 one: the two heaviest chains (records, the first qm wave) get a
-// SIMD of their own, the others pair up.
-constexpr int PX_WF = 8, PX_WQ = 9, PX_WR = 10;   // F, Q, R
+constexpr int PX_NB = 7;              // interior-loop blocks (waves 0..6)
+constexpr int PX_NMW = 4;             // qm item waves
+// Roles of waves 7-13 (seven interior-loop waves, four qm waves: the qm wave
+// with the most items sets the step at a power-of-two lane split, so a fourth
+// qm wave halves it at about half of the spans; measured +1 % over 8 + 3).
+constexpr int PX_WF = 7, PX_WQ = 8, PX_WR = 9;   // F, Q, R
 __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most items) or -1
-    return w == 11 ? 0 : w == 13 ? 1 : w == 12 ? 2 : -1;
+    return w == 10 ? 0 : w == 11 ? 1 : w == 13 ? 2 : w == 12 ? 3 : -1;
 }
 constexpr int PX_NMAX = 100;
 constexpr int PX_RF = 8;              // record fields (rec_store): word, mmo, mo, m23, 1x1..2x2 factors
@@ -647,7 +646,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     __syncthreads();
     PSTAMP(0);
 
-    // ---- records (wave 10): the changed pairable cells of diagonal D (rank
+    // ---- records (wave 9): the changed pairable cells of diagonal D (rank
     // lists) and their setup values -- outer factors of the closing pair, the
     // unpaired runs, the 1x1..2x2 table factors (HBM/L2 loads) -- gathered at step
     // D - 2 (rec_load) and written at step D - 1 (rec_store), so the table loads
@@ -780,15 +779,13 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         switch (wid) {
             // blocks of about equal LDS cost per lane-set (a size >= 6: 3 reads for
             // its special shapes + one per 4 generic ones; the small sizes ~3 per shape)
-            // (the heavier blocks on waves 2, 3, 6, 7: SIMDs 1 and 3 host one other role each)
-            case 0: pb_sweep<26, 25, 3, 8, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 1: pb_sweep<28, 27, 2, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 2: pb_sweep<30, 29, 0, 1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 3: pb_sweep<24, 23, 4, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 4: pb_sweep<18, 17, 10, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 5: pb_sweep<20, 19, 9, 6, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 6: pb_sweep<22, 21, 5, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            default: pb_sweep<16, 15, 14, 13, 12>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 0: pb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 2: pb_sweep<3, 20, 18, 8, 6>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<28, 26, 1, 9, 7>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 14, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            default: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
     } else {
         // the M / F / Q / R chains set the step time; issue arbitration favours the
