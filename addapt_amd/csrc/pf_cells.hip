@@ -469,26 +469,25 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
     auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
 
-    // ---- refold restore first: its HBM loads overlap the rest of the setup
+    // ---- refold restore: every table from the current slot (the changed cells are
+    // recomputed over it), two cells per lane and load, both folds interleaved.
+    // The loads are issued here and stored to LDS after the motif scan, so their
+    // HBM latency overlaps the rest of the setup.  (HBM side dword-aligned only
+    // when cells or B1 are odd: fine for global loads.)
+    constexpr int RS = 8;   // loads per lane: 3 * C / 2 <= RS * PX_NT for N <= PX_NMAX
+    static_assert(3 * (((PX_NMAX - 4) * (PX_NMAX - 3) / 2) / 2) <= RS * PX_NT, "restore loads fit RS per lane");
+    const int half = C >> 1;
+    float2 rsx[RS], rsy[RS];
     if (incr) {
-        // refold: every table from the current slot (the changed cells are
-        // recomputed over it), two cells per lane and load, both folds interleaved
-        // (HBM side dword-aligned only when cells or B1 are odd: fine for global loads)
-        float4 *qd = reinterpret_cast<float4 *>(L.qb);   // qb, qm, q1 contiguous at a16(C + slack) strides
-        const int half = C >> 1;
-        const size_t ls4 = (Y.QM - Y.QB) >> 4;
-#pragma unroll 8   // N = 100: every load of a lane in flight at once
-        for (int k = tid; k < 3 * half; k += PX_NT) {
-            const int a = k / half, c = k - a * half;
+#pragma unroll
+        for (int t = 0; t < RS; t++) {
+            const int k = tid + t * PX_NT;
+            const int kk = k < 3 * half ? k : 0;
+            const int a = kk / half, c = kk - a * half;
             const float *sa = src + a * Cs + 2 * c;
-            const float2 x = *reinterpret_cast<const float2 *>(sa), y = *reinterpret_cast<const float2 *>(sa + B1);
-            qd[a * ls4 + c] = float4{x.x, y.x, x.y, y.y};
+            rsx[t] = *reinterpret_cast<const float2 *>(sa);
+            rsy[t] = *reinterpret_cast<const float2 *>(sa + B1);
         }
-        if (C & 1)
-            for (int a = tid; a < 3; a += PX_NT) {
-                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
-            }
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
     } else {
         for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
     }
@@ -572,6 +571,23 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             const bool all = __ballot(!ok) == 0;
             if (lane == 0) L.mat[o] = all ? 1 : 0;
         }
+    }
+    if (incr) {   // the restore's stores (loads issued at the start)
+        float4 *qd = reinterpret_cast<float4 *>(L.qb);   // qb, qm, q1 contiguous at a16(C + slack) strides
+        const size_t ls4 = (Y.QM - Y.QB) >> 4;
+#pragma unroll
+        for (int t = 0; t < RS; t++) {
+            const int k = tid + t * PX_NT;
+            if (k < 3 * half) {
+                const int a = k / half, c = k - a * half;
+                qd[a * ls4 + c] = float4{rsx[t].x, rsy[t].x, rsx[t].y, rsy[t].y};
+            }
+        }
+        if (C & 1)
+            for (int a = tid; a < 3; a += PX_NT) {
+                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
+            }
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
     }
     __syncthreads();
     const uint8_t *S = L.S;
