@@ -557,27 +557,31 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             L.mat[o] = ok ? 1 : 0;
         }
     }
-    __syncthreads();
-    for (int k = tid; k < OX_WIN * L.RL; k += OX_NT) {
-        L.qw[k] = 0.f;
-        L.ow[k] = 0;
-    }
-    for (int k = tid; k < C; k += OX_NT) L.yc[k] = 0.f;
-    // the pairable cells of every diagonal in rank order (the B lanes; an
-    // unconstrained fold: the pair type alone decides)
-    for (int D = 4 + wid; D <= N - 1; D += OX_NW) {
-        const int od = off(D, N);
-        int base = 0;
-        for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
-            const int i = i0 + lane;
-            const bool pr = i <= N - D && ptype(S[i], S[i + D]) != 0;
-            const uint64_t m = __ballot(pr);
-            const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-            if (pr) L.cl[od + slot] = uint8_t(i);
-            base += __popcll(m);
+    // while wave 0 runs the exterior adjoint: the window zeroed and the pairable
+    // cells of every diagonal in rank order (the B lanes; an unconstrained fold:
+    // the pair type alone decides), on waves 2.. (neither touches G)
+    if (wid >= 2) {
+        const int t2 = tid - 2 * WAVE, n2 = OX_NT - 2 * WAVE;
+        for (int k = t2; k < OX_WIN * L.RL; k += n2) {
+            L.qw[k] = 0.f;
+            L.ow[k] = 0;
         }
-        if (lane == 0) cn[D] = uint8_t(base);
+        for (int D = 4 + wid - 2; D <= N - 1; D += OX_NW - 2) {
+            const int od = off(D, N);
+            int base = 0;
+            for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
+                const int i = i0 + lane;
+                const bool pr = i <= N - D && ptype(S[i], S[i + D]) != 0;
+                const uint64_t m = __ballot(pr);
+                const int slot = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                if (pr) L.cl[od + slot] = uint8_t(i);
+                base += __popcll(m);
+            }
+            if (lane == 0) cn[D] = uint8_t(base);
+        }
     }
+    __syncthreads();
+    for (int k = tid; k < C; k += OX_NT) L.yc[k] = 0.f;   // G's region: Y column-major from here on
     __syncthreads();
 
     OSTAMP(1);   // exterior adjoint + zeroing
