@@ -145,13 +145,20 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
             "reference_2016_per_core": 14.4}
 
 
-def pf_kernel_label(bppm):
-    """The PF kernels of one step's score window (kernels.hip launch_score_m / launch_steps)."""
-    inside = ("score_kernel<SumProd> (lanes = terms)" if os.environ.get("ADX_PF_KERNEL") == "rows"
+def pf_kernel_label(bppm, length=100):
+    """The PF kernels of one step's score window (kernels.hip launch_score_m / launch_steps):
+    pf_cells_kernel up to N = 100 (pf_cells.hip PX_NMAX), outside_cells_kernel up to
+    N = 112 (outside_cells.hip OX_NMAX), the general kernels beyond (their LDS)."""
+    inside = ("score_kernel<SumProd> (lanes = terms)"
+              if os.environ.get("ADX_PF_KERNEL") == "rows" or length > 100
               else "pf_cells_kernel (lanes = cells)")
     if bppm:
-        return inside + " + outside_cells_kernel + combine_kernel (one event window per step)"
+        return inside + " + %s + combine_kernel (one event window per step)" % outside_kernel(length)
     return inside + " + combine_kernel"
+
+
+def outside_kernel(length):
+    return "outside_cells_kernel" if length <= 112 else "bppm_kernel<512, GOUT>"
 
 
 def mfe_kernel_label():
@@ -290,7 +297,7 @@ def main():
             tj = json.load(f)
         traffic = tj.get("bytes_per_launch")
         if a.bppm:   # the dominant kernel's own bytes (the summary holds every kernel of the window)
-            own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if "outside_cells_kernel" in name]
+            own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if outside_kernel(a.length).split("<")[0] in name]
             traffic = own[0] if own else None
         traffic_src = os.path.relpath(a.traffic_json, ROOT)
     peak, peak_note = roofline.valu_peak(a.fold)
@@ -302,9 +309,9 @@ def main():
         "frac": (achieved_tflops / peak) if achieved_tflops else None,
         "traffic": traffic,
         "compute_unit": peak_note,
-        "kernel": ("outside_cells_kernel (events around its launch; the window also holds "
-                   + pf_kernel_label(False) + ")") if a.bppm
-                  else mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(False),
+        "kernel": (outside_kernel(a.length) + " (events around its launch; the window also holds "
+                   + pf_kernel_label(False, a.length) + ")") if a.bppm
+                  else mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(False, a.length),
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": kern_ms,
         "window_ms_per_launch": score_ms,
