@@ -1240,7 +1240,7 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
 }
 
 template <int NT, int P, class SR>
-__global__ void __launch_bounds__(NT, (NT > 512) ? 3 : (P == 2 ? 2 : 4))   // min waves per SIMD
+__global__ void __launch_bounds__(NT, (NT >= 1024) ? 4 : (NT > 512) ? 3 : (P == 2 ? 2 : 4))   // min waves per SIMD
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
              double *terms, float *dG, const int *mask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1974,6 +1974,10 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         return hipGetLastError();
     }
     if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
+    // one workgroup per CU (N = 150: the P = 1 tables take most of the LDS): 16
+    // waves instead of 8 (the same 128 VGPRs a lane)
+    if (2 * lds_size<1, 512>(ka, 0, false) > size_t(LDS_LIMIT) - 2048)
+        return launch_score_t<1024, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
     return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
 }
 
@@ -2005,7 +2009,7 @@ template <bool GOUT>
 static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs, int W, const int *mask,
                                 double *full, int ld, double *pair_p, char *scratch, hipStream_t stream,
                                 bool reuse) {
-    auto k = bppm_kernel<512, GOUT>;
+    auto k = bppm_kernel<GOUT ? 1024 : 512, GOUT>;   // GOUT (N = 150): one workgroup per CU, 16 waves
     static size_t configured = 0;
     if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
@@ -2013,7 +2017,7 @@ static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs
         if (e != hipSuccess) return e;
         configured = lds;
     }
-    hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p,
+    hipLaunchKernelGGL(k, dim3(W * ka.n_bvars), dim3(GOUT ? 1024 : 512), lds, stream, ka, ka.X, seqs, W, mask, full, ld, pair_p,
                        scratch, choose_p(ka), reuse ? 1 : 0);
     return hipGetLastError();
 }
