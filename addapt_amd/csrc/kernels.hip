@@ -1288,16 +1288,16 @@ struct Outs {
     float *qbb;    // diagonal-major: qbb(i,j) * mismatchI(outer code), 0 for non-pairable cells
     float *qmb;    // column-major colb(j)+i-1
     float *Y;      // row-major rowb(i)+j-i-4
-    uint8_t *oc;   // diagonal-major outer code type*25 + S[i+1]*5 + S[j-1]
     float *qm1b;   // [2][NP] the last two diagonals, by i
     float *q5b;    // [NP]
     float *pm;     // [NP] motif site weights qbb(o, o+L-1) * extra / Z, by site start
 };
 
-// LDS carve of the outside arrays after the inside layout.  GOUT: the four
-// cell tables live in a per-workgroup global scratch slice instead (devices
-// whose inside + outside tables exceed one CU's LDS, e.g. N = 150); the rest
-// stays in LDS.
+// LDS carve of the outside arrays after the inside layout.  GOUT: the three
+// cell tables (qbb, qmb, Y) live in a per-workgroup global scratch slice
+// instead (devices whose inside + outside tables exceed one CU's LDS, e.g.
+// N = 150); the rest stays in LDS.  (A column-major copy of Y for coalesced
+// r2 reads was measured slower: 58.4 vs 53.7 ms at N = 150.)
 template <bool DRY, bool GOUT>
 __host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, int Nmax, Outs *O,
                                               char *gbase = nullptr) {
@@ -1318,7 +1318,6 @@ __host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, i
     t.qbb = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
     t.qmb = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
     t.Y = reinterpret_cast<float *>(GOUT ? gtake(C * 4) : take(C * 4));
-    t.oc = reinterpret_cast<uint8_t *>(GOUT ? gtake(C) : take(C));
     t.qm1b = reinterpret_cast<float *>(take(2 * NP * 4));
     t.q5b = reinterpret_cast<float *>(take(NP * 4));
     t.pm = reinterpret_cast<float *>(take(NP * 4));
@@ -1327,7 +1326,7 @@ __host__ __device__ inline size_t outs_layout(char *base, size_t o, int cells, i
 }
 // global scratch bytes per workgroup of the GOUT layout
 __host__ __device__ inline size_t outs_global_bytes(int cells) {
-    return 3 * ((size_t(cells) * 4 + 15) & ~size_t(15)) + ((size_t(cells) + 15) & ~size_t(15));
+    return 3 * ((size_t(cells) * 4 + 15) & ~size_t(15));
 }
 
 // full: row stride ld (folded coordinates, 0-based), pre-zeroed by the host;
@@ -1351,13 +1350,14 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
     const bool motif = V.motif != 0 && XS->motif_len > 0;
     const int mL = XS->motif_len;
     const DevTables &T = *ka.T;
+    // outer code of pair (a, b): type * 25 + S[a+1] * 5 + S[b-1]
+    auto ocode = [&](int a, int b) { return ptype(S[a], S[b]) * 25 + S[a + 1] * 5 + S[b - 1]; };
 
-    // ---- setup: outer codes, zeroed adjoints
+    // ---- setup: zeroed adjoints
     for (int dd = 4 + wid; dd <= N - 1; dd += NW) {
         const int od = off(dd, N);
         for (int r = lane; r < N - dd; r += WAVE) {
             const int i = r + 1, j = i + dd;
-            O.oc[od + r] = static_cast<uint8_t>(ptype(S[i], S[j]) * 25 + S[i + 1] * 5 + S[j - 1]);
             O.qbb[od + r] = 0.f;
             O.qmb[colb(j) + i - 1] = 0.f;
             O.Y[rowb(i, N) + dd - 4] = 0.f;
@@ -1459,7 +1459,7 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                     if (k >= 0 && u <= umax && n1 <= A && n2 <= B) {
                         const int a = i - 1 - n1, b = j + 1 + n2;
                         const int oidx = off(d + 2 + u, N) + a - 1;
-                        const int ocd = O.oc[oidx];
+                        const int ocd = ocode(a, b);   // from S (no dependent scratch load)
                         const int t1 = (ocd * 41) >> 10;
                         // select form of the qb_terms factors (no divergent branches):
                         // base (outer code) x second table factor x uniform inner factor
@@ -1503,7 +1503,7 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                 const float ext = L.dt[DT_EXT + ty * 36 + ((i > 1) ? S[i - 1] : 5) * 6 + ((j < N) ? S[j + 1] : 5)];
                 const float stem = L.dt[DT_MLS + ty * 25 + S[i - 1] * 5 + S[j + 1]];
                 const float qbb_v = v_int + O.q5b[j] * L.q5[0][i - 1] * ext + qm1b_v * stem;
-                qbbm = qbb_v * L.dt[DT_MMI + O.oc[idx]];
+                qbbm = qbb_v * L.dt[DT_MMI + ocode(i, j)];
                 if (d - 2 >= 4)   // X(i+1, j-1): this pair closing a multiloop
                     O.Y[rowb(i + 1, N) + d - 6] =
                         qbb_v * mlclosing * L.dt[DT_MLS + rtype(ty) * 25 + S[j - 1] * 5 + S[i + 1]];
@@ -1542,7 +1542,7 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                 const int idx = off(j - i, N) + i - 1;
                 if (!SumProd::is_mark(L.qbm[0][idx])) {
                     const double qb = double(L.qbm[0][idx]) * double(ct[CT_INVMM + L.cc[idx]]);
-                    const double qbb = double(O.qbb[idx]) / double(L.dt[DT_MMI + O.oc[idx]]);
+                    const double qbb = double(O.qbb[idx]) / double(L.dt[DT_MMI + ocode(i, j)]);
                     pij = qb * qbb / double(Z);
                 }
                 if (motif)
