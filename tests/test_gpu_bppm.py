@@ -180,3 +180,25 @@ def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
             if ref["outcome"][s] != 2:
                 a, b = tr["proposed_score"][s, w], ref["proposed_score"][s]
                 assert a == b or abs(a - b) <= 2e-3 * max(1.0, abs(b)), (N, w, s, a, b)
+
+
+@pytest.mark.parametrize("N", [100, 150])
+def test_mc_pair_terms_full_size(native, oracle, N):
+    """Configs 3 / 4 at their per-GPU size (4096 walkers; N = 100: pf_cells +
+    outside_cells, N = 150: the 16-wave score_kernel + bppm_kernel): counters sum
+    to the steps, and sampled walkers' final scores (pair probabilities
+    included) equal the oracle's from-scratch scores of their final sequences."""
+    tmpl, active = workloads.synthetic(N)
+    terms = _objective(N)
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    W = 4096
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(2)
+    final, scores, counters = eng.download()
+    assert (counters.sum(axis=1) == 2).all()
+    sf = _oracle_sf(oracle, terms)
+    for w in list(range(0, W, 683)) + [W - 1]:
+        ref, _ = sf.score(final[w], [active])
+        assert abs(scores[w] - ref) <= 2e-3 * max(1.0, abs(ref)), (N, w, scores[w], ref)
