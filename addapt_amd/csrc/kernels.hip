@@ -1423,15 +1423,48 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
             const int i = r + 1, j = i + d;
             const int idx = od + r;
             const bool pr = !SumProd::is_mark(L.qbm[0][idx]);
-            // multiloop adjoints: split points over lanes
+            // multiloop adjoints: split points over lanes.  Every read below is
+            // unconditional (a masked lane reads a valid cell and discards it by a
+            // select): a read under a per-lane branch waits for memory before the
+            // next one issues, and with the outside tables in global scratch
+            // (GOUT) each wait is a global-memory round trip.
             float a_qmb = 0.f, a_rest = 0.f;
-            for (int l = j + 5 + lane; l <= N; l += WAVE)
-                a_qmb = fmaf(O.Y[rowb(i, N) + l - i - 4], L.qm1[0][colb(l) + j], a_qmb);
-            for (int ip = 1 + lane; ip < i; ip += WAVE) {
-                const int t = i - ip;
-                float x = (L.up[ip] >= t) ? O.qmb[colb(j) + ip - 1] * L.pw[t] : 0.f;
-                if (t >= 5) x = fmaf(O.Y[rowb(ip, N) + j - ip - 4], L.qm[0][rowb(ip, N) + t - 5], x);
-                a_rest += x;
+            for (int l0 = j + 5; l0 <= N; l0 += 2 * WAVE) {
+                float y[2], q[2];
+                bool ok[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int l = l0 + h * WAVE + lane;
+                    ok[h] = l <= N;
+                    y[h] = O.Y[ok[h] ? rowb(i, N) + l - i - 4 : 0];
+                    q[h] = L.qm1[0][ok[h] ? colb(l) + j : 0];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) a_qmb = ok[h] ? fmaf(y[h], q[h], a_qmb) : a_qmb;
+            }
+            for (int p0 = 1; p0 < i; p0 += 2 * WAVE) {
+                float qv[2], yv[2], mv[2], pv[2];
+                int t[2];
+                bool ok[2], up[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int ip = p0 + h * WAVE + lane;
+                    ok[h] = ip < i;
+                    t[h] = i - ip;
+                    const int ips = ok[h] ? ip : 1, ts = ok[h] ? t[h] : 0;
+                    const bool l5 = ok[h] && t[h] >= 5;
+                    qv[h] = O.qmb[colb(j) + ips - 1];
+                    pv[h] = L.pw[ts];
+                    up[h] = L.up[ips] >= ts;
+                    yv[h] = O.Y[l5 ? rowb(ip, N) + j - ip - 4 : 0];
+                    mv[h] = L.qm[0][l5 ? rowb(ip, N) + t[h] - 5 : 0];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    float x = up[h] ? qv[h] * pv[h] : 0.f;
+                    x = t[h] >= 5 ? fmaf(yv[h], mv[h], x) : x;
+                    a_rest = ok[h] ? a_rest + x : a_rest;
+                }
             }
             // interior loops (p, q) = (i, j) inside (a, b) = (i-1-n1, j+1+n2)
             float a_int = 0.f;
@@ -1443,41 +1476,46 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                 const float mo_in = ct[CT_ONEN + ccode] * mmin;
                 const float m23_in = ct[CT_M23O + ccode];
                 const int A = min(int(L.dn[i - 1]), i - 2), B = min(int(L.up[j + 1]), N - 1 - j);
-                float g = 0.f;
+                float gv[GSLOTS];
+                bool gok[GSLOTS];
 #pragma unroll
                 for (int s = 0; s < GSLOTS; s++) {
                     const int n1 = gn1[s], u = gu[s], n2 = u - n1;
-                    if (u <= umax && n1 <= A && n2 <= B) {
-                        const int oidx = off(d + 2 + u, N) + i - 2 - n1;
-                        g = fmaf(O.qbb[oidx], gfv[s], g);
-                    }
+                    gok[s] = u <= umax && n1 <= A && n2 <= B;
+                    gv[s] = O.qbb[gok[s] ? off(d + 2 + u, N) + i - 2 - n1 : idx];
                 }
-                float sp = 0.f;
+                float sv[SSLOTS], stv[SSLOTS], sf[SSLOTS];
+                bool sok[SSLOTS], stab[SSLOTS];
 #pragma unroll
                 for (int s = 0; s < SSLOTS; s++) {
                     const int n1 = sn1[s], n2 = sn2[s], k = skd[s], u = n1 + n2;
-                    if (k >= 0 && u <= umax && n1 <= A && n2 <= B) {
-                        const int a = i - 1 - n1, b = j + 1 + n2;
-                        const int oidx = off(d + 2 + u, N) + a - 1;
-                        const int ocd = ocode(a, b);   // from S (no dependent scratch load)
-                        const int t1 = (ocd * 41) >> 10;
-                        // select form of the qb_terms factors (no divergent branches):
-                        // base (outer code) x second table factor x uniform inner factor
-                        const int base = (k == TK_BUL) ? CT_BUL : (k == TK_1N) ? CT_ONEN : CT_INVMM;
-                        const int sec = (k <= TK_B1) ? CT_STK + t1 * 8 + ty2 : (k == TK_M23) ? CT_M23O + ocd : CT_ONE;
-                        float um = (k == TK_BUL) ? tau_in : (k == TK_1N) ? mo_in : (k == TK_M23) ? m23_in : 1.f;
-                        if (k >= TK_I11 && k <= TK_I22) {   // 1x1, 1x2, 2x1, 2x2 tables (HBM / L2)
-                            const int a1 = S[a + 1], b1 = S[b - 1], sp1 = S[i - 1], sq1 = S[j + 1];
-                            const float *src;
-                            if (k == TK_I11) src = &T.int11[t1][ty2][a1][b1];
-                            else if (k == TK_I12) src = &T.int21[t1][ty2][a1][sq1][b1];
-                            else if (k == TK_I21) src = &T.int21[ty2][t1][sq1][a1][sp1];
-                            else src = &T.int22[t1][ty2][a1][sp1][sq1][b1];
-                            um = *src;
-                        }
-                        sp = fmaf(O.qbb[oidx], ct[base + ocd] * ct[sec] * (um * sfv[s]), sp);
-                    }
+                    sok[s] = k >= 0 && u <= umax && n1 <= A && n2 <= B;
+                    const int a = sok[s] ? i - 1 - n1 : i, b = sok[s] ? j + 1 + n2 : j;   // masked: the cell itself
+                    sv[s] = O.qbb[sok[s] ? off(d + 2 + u, N) + a - 1 : idx];
+                    const int ocd = ocode(a, b);   // from S (no dependent scratch load)
+                    const int t1 = (ocd * 41) >> 10;
+                    // select form of the qb_terms factors (no divergent branches):
+                    // base (outer code) x second table factor x uniform inner factor
+                    const int base = (k == TK_BUL) ? CT_BUL : (k == TK_1N) ? CT_ONEN : CT_INVMM;
+                    const int sec = (k <= TK_B1) ? CT_STK + t1 * 8 + ty2 : (k == TK_M23) ? CT_M23O + ocd : CT_ONE;
+                    const float um = (k == TK_BUL) ? tau_in : (k == TK_1N) ? mo_in : (k == TK_M23) ? m23_in : 1.f;
+                    // 1x1, 1x2, 2x1, 2x2 tables (HBM / L2): the address selected, the load unconditional
+                    const int a1 = S[a + 1], b1 = S[b - 1], sp1 = S[i - 1], sq1 = S[j + 1];
+                    const float *src = (k == TK_I11) ? &T.int11[t1][ty2][a1][b1]
+                                     : (k == TK_I12) ? &T.int21[t1][ty2][a1][sq1][b1]
+                                     : (k == TK_I21) ? &T.int21[ty2][t1][sq1][a1][sp1]
+                                     : &T.int22[t1][ty2][a1][sp1][sq1][b1];
+                    stab[s] = k >= TK_I11 && k <= TK_I22;
+                    stv[s] = *src;
+                    sf[s] = ct[base + ocd] * ct[sec] * um;
                 }
+                float g = 0.f;
+#pragma unroll
+                for (int s = 0; s < GSLOTS; s++) g = gok[s] ? fmaf(gv[s], gfv[s], g) : g;
+                float sp = 0.f;
+#pragma unroll
+                for (int s = 0; s < SSLOTS; s++)
+                    sp = sok[s] ? fmaf(sv[s], sf[s] * ((stab[s] ? stv[s] : 1.f) * sfv[s]), sp) : sp;
                 a_int = fmaf(g, mmin, sp);
             }
             float s_qmb, s_rest;
