@@ -1429,43 +1429,50 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
             // next one issues, and with the outside tables in global scratch
             // (GOUT) each wait is a global-memory round trip.
             float a_qmb = 0.f, a_rest = 0.f;
-            for (int l0 = j + 5; l0 <= N; l0 += 2 * WAVE) {
-                float y[2], q[2];
-                bool ok[2];
+            struct MlQ { float y[2], q[2]; bool ok[2]; };
+            struct MlR { float qv[2], yv[2], mv[2], pv[2]; int t[2]; bool ok[2], up[2]; };
+            auto q_load = [&](int l0, MlQ &m) {   // qmb split points l0 + lane, l0 + 64 + lane
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int l = l0 + h * WAVE + lane;
-                    ok[h] = l <= N;
-                    y[h] = O.Y[ok[h] ? rowb(i, N) + l - i - 4 : 0];
-                    q[h] = L.qm1[0][ok[h] ? colb(l) + j : 0];
+                    m.ok[h] = l <= N;
+                    m.y[h] = O.Y[m.ok[h] ? rowb(i, N) + l - i - 4 : 0];
+                    m.q[h] = L.qm1[0][m.ok[h] ? colb(l) + j : 0];
                 }
+            };
+            auto q_acc = [&](const MlQ &m) {
 #pragma unroll
-                for (int h = 0; h < 2; h++) a_qmb = ok[h] ? fmaf(y[h], q[h], a_qmb) : a_qmb;
-            }
-            for (int p0 = 1; p0 < i; p0 += 2 * WAVE) {
-                float qv[2], yv[2], mv[2], pv[2];
-                int t[2];
-                bool ok[2], up[2];
+                for (int h = 0; h < 2; h++) a_qmb = m.ok[h] ? fmaf(m.y[h], m.q[h], a_qmb) : a_qmb;
+            };
+            auto r_load = [&](int p0, MlR &m) {   // r2 / qmb-chain split points p0 + lane, p0 + 64 + lane
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int ip = p0 + h * WAVE + lane;
-                    ok[h] = ip < i;
-                    t[h] = i - ip;
-                    const int ips = ok[h] ? ip : 1, ts = ok[h] ? t[h] : 0;
-                    const bool l5 = ok[h] && t[h] >= 5;
-                    qv[h] = O.qmb[colb(j) + ips - 1];
-                    pv[h] = L.pw[ts];
-                    up[h] = L.up[ips] >= ts;
-                    yv[h] = O.Y[l5 ? rowb(ip, N) + j - ip - 4 : 0];
-                    mv[h] = L.qm[0][l5 ? rowb(ip, N) + t[h] - 5 : 0];
+                    m.ok[h] = ip < i;
+                    m.t[h] = i - ip;
+                    const int ips = m.ok[h] ? ip : 1, ts = m.ok[h] ? m.t[h] : 0;
+                    const bool l5 = m.ok[h] && m.t[h] >= 5;
+                    m.qv[h] = O.qmb[colb(j) + ips - 1];
+                    m.pv[h] = L.pw[ts];
+                    m.up[h] = L.up[ips] >= ts;
+                    m.yv[h] = O.Y[l5 ? rowb(ip, N) + j - ip - 4 : 0];
+                    m.mv[h] = L.qm[0][l5 ? rowb(ip, N) + m.t[h] - 5 : 0];
                 }
+            };
+            auto r_acc = [&](const MlR &m) {
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    float x = up[h] ? qv[h] * pv[h] : 0.f;
-                    x = t[h] >= 5 ? fmaf(yv[h], mv[h], x) : x;
-                    a_rest = ok[h] ? a_rest + x : a_rest;
+                    float x = m.up[h] ? m.qv[h] * m.pv[h] : 0.f;
+                    x = m.t[h] >= 5 ? fmaf(m.yv[h], m.mv[h], x) : x;
+                    a_rest = m.ok[h] ? a_rest + x : a_rest;
                 }
-            }
+            };
+            // the first 128 split points of both sums are read before the interior
+            // loops and summed after them (one batch of reads per cell at N <= 133)
+            MlQ mq;
+            MlR mr;
+            q_load(j + 5, mq);
+            r_load(1, mr);
             // interior loops (p, q) = (i, j) inside (a, b) = (i-1-n1, j+1+n2)
             float a_int = 0.f;
             if (pr) {
@@ -1517,6 +1524,16 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
                 for (int s = 0; s < SSLOTS; s++)
                     sp = sok[s] ? fmaf(sv[s], sf[s] * ((stab[s] ? stv[s] : 1.f) * sfv[s]), sp) : sp;
                 a_int = fmaf(g, mmin, sp);
+            }
+            q_acc(mq);
+            for (int l0 = j + 5 + 2 * WAVE; l0 <= N; l0 += 2 * WAVE) {
+                q_load(l0, mq);
+                q_acc(mq);
+            }
+            r_acc(mr);
+            for (int p0 = 1 + 2 * WAVE; p0 < i; p0 += 2 * WAVE) {
+                r_load(p0, mr);
+                r_acc(mr);
             }
             float s_qmb, s_rest;
             wave_sum2<SumProd>(a_qmb, a_rest, s_qmb, s_rest);
