@@ -1418,6 +1418,14 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
         // cells r = wid + k*NW of this wave: lane k keeps cell k's three sums and
         // finishes it in the parallel tail below
         float v_qmb = 0.f, v_rest = 0.f, v_int = 0.f;
+        // Y(i, j) of the lane's tail cell (X(i, j), stored two diagonals ago; no
+        // wave writes span d before the tail), read now so the tail's update is a store
+        float y_old;
+        {
+            const int kc = (nc - wid + NW - 1) / NW;
+            const int i = lane < kc ? wid + lane * NW + 1 : 1;
+            y_old = O.Y[lane < kc ? rowb(i, N) + d - 4 : 0];
+        }
         int k = 0;
         for (int r = wid; r < nc; r += NW, k++) {
             const int i = r + 1, j = i + d;
@@ -1550,7 +1558,7 @@ __device__ void outside(const KArgs &ka, int v, int bv, const Lds<1> &L, const O
             const float chain = (j < N && L.up[j + 1] >= 1) ? mlbase_sig * O.qm1b[((d + 1) & 1) * NP + i] : 0.f;
             const float qm1b_v = v_qmb + v_rest + chain;
             O.qmb[colb(j) + i - 1] = v_qmb;
-            O.Y[rowb(i, N) + d - 4] += v_qmb;     // X(i, j) was stored two diagonals ago
+            O.Y[rowb(i, N) + d - 4] = y_old + v_qmb;   // X(i, j) + qmb(i, j)
             O.qm1b[(d & 1) * NP + i] = qm1b_v;
             float qbbm = 0.f;
             if (pr) {
