@@ -2037,10 +2037,10 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         return hipGetLastError();
     }
     if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
-    // one workgroup per CU (N = 150: the P = 1 tables take most of the LDS): 16
-    // waves instead of 8 (the same 128 VGPRs a lane)
+    // one workgroup per CU (N = 150: the P = 1 tables take most of the LDS): 12
+    // waves instead of 8, 168 VGPRs a lane (16 waves at 128 spill: 29.9 vs 28.2 ms)
     if (2 * lds_size<1, 512>(ka, 0, false) > size_t(LDS_LIMIT) - 2048)
-        return launch_score_t<1024, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
+        return launch_score_t<768, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
     return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
 }
 
@@ -2072,7 +2072,7 @@ template <bool GOUT>
 static hipError_t launch_bppm_t(const KArgs &ka, size_t lds, const uint8_t *seqs, int W, const int *mask,
                                 double *full, int ld, double *pair_p, char *scratch, hipStream_t stream,
                                 bool reuse) {
-    auto k = bppm_kernel<GOUT ? 1024 : 512, GOUT>;   // GOUT (N = 150): one workgroup per CU, 16 waves
+    auto k = bppm_kernel<GOUT ? 1024 : 512, GOUT>;   // GOUT (N = 150): one workgroup per CU, 16 waves (12: 50.1 vs 49.1 ms)
     static size_t configured = 0;
     if (lds > configured) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
