@@ -141,7 +141,7 @@ void build_tables(const EnergyParams &P, DevTables &T, bool mfe) {
 struct Motif {
     std::string seq, fold;
     double energy_kcal = 0.0;
-    int mode = ADX_MOTIF_AUTO;
+    int mode = ADX_MOTIF_ADD;
     bool present = false;
 };
 

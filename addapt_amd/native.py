@@ -223,7 +223,7 @@ class Engine:
     """
 
     def __init__(self, sequence, macrostates, terms, aptamer=None, thermostat=None, contexts=None,
-                 motif_mode=MOTIF_AUTO, params=None, device=0, fold_mode="pf"):
+                 motif_mode=MOTIF_ADD, params=None, device=0, fold_mode="pf"):
         self.params = params or default_params()
         self.N = len(sequence)
         d = RunDesc()

@@ -123,12 +123,14 @@ typedef struct adx_thermostat {
     double t_init;
 } adx_thermostat;
 
-#define ADX_MOTIF_ADD 0        /* ligand bonus added to the motif structure */
-#define ADX_MOTIF_REPLACE 1    /* motif structure's total energy := bonus */
-#define ADX_MOTIF_AUTO 2       /* default: ADD in partition functions (pinned by the
-                                  ensemble dG annotations, test_scoring.cc:52-55),
-                                  REPLACE in the MFE (pinned by the holo MFE
-                                  annotation -9.22, test_scoring.cc:154) */
+#define ADX_MOTIF_ADD 0        /* default, both fold modes: ligand bonus added to the motif
+                                  structure's own loop energies (one soft constraint for PF
+                                  and MFE, as vrna_sc_add_hi_motif is one call, scoring.cc:94;
+                                  pinned by the rhf(6) ensemble annotations, test_scoring.cc:54-55) */
+#define ADX_MOTIF_REPLACE 1    /* opt-in: motif structure's total energy := bonus */
+#define ADX_MOTIF_AUTO 2       /* opt-in: ADD in partition functions, REPLACE in MFE folds --
+                                  reproduces RNAfold's printed holo MFE -9.22
+                                  (test_scoring.cc:154) as well as the ensemble */
 
 #define ADX_FOLD_PF 0          /* MacrostateProbTerm over vrna_pf ensembles (scoring.cc:53-71) */
 #define ADX_FOLD_MFE 1         /* the same terms over minimum free energies:
@@ -149,7 +151,7 @@ typedef struct adx_run_desc {
     const char *aptamer_seq;         /* NULL: no aptamer (holo folds like apo) */
     const char *aptamer_fold;
     double aptamer_energy_kcal;      /* kT*ln(Kd/1M) (scoring.cc:91-99) */
-    int motif_mode;                  /* ADX_MOTIF_ADD / _REPLACE / _AUTO (recommended) */
+    int motif_mode;                  /* ADX_MOTIF_ADD (default, 0) / _REPLACE / _AUTO */
     int n_contexts;                  /* 0 = none; else map (name) order */
     const adx_context_desc *contexts;
     adx_thermostat thermostat;

@@ -257,9 +257,11 @@ static int model_init(model_t *m, const orc_params *P, const char *seq, const ch
         free(stk);
         double eint = orc_eval_structure(P, motif->seq, motif->fold); /* kcal */
         m->m_Eint = eint;
-        /* mode 2 (auto): ADD for partition functions, REPLACE for the MFE --
-         * the conventions the reference's two RNAfold annotations pin
-         * (ensemble dG test_scoring.cc:52-55, holo MFE test_scoring.cc:154) */
+        /* mode 0 (ADD, the default): bonus + the motif's own loops in both fold
+         * modes (the ensemble annotations, test_scoring.cc:54-55); mode 1
+         * (REPLACE): motif energy := bonus; mode 2 (AUTO, opt-in): ADD for
+         * partition functions, REPLACE for the MFE -- also reproduces the printed
+         * holo MFE -9.22 (test_scoring.cc:154) */
         double beff = motif->mode == 1 ? motif->energy_kcal - eint : motif->energy_kcal;
         double beff_mfe = motif->mode == 0 ? motif->energy_kcal : motif->energy_kcal - eint;
         m->m_extra = boltz(eint * 100.0) * (boltz(beff * 100.0) - 1.0);

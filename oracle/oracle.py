@@ -149,7 +149,8 @@ def default_params():
     return _default_params
 
 
-def make_motif(seq, fold, energy_kcal, mode=2):
+def make_motif(seq, fold, energy_kcal, mode=0):
+    """mode 0 = ADD (default, as the engine), 1 = REPLACE, 2 = AUTO (ADD in PF, REPLACE in MFE)."""
     m = Motif(_b(seq), _b(fold), energy_kcal, mode)
     m._keep = (seq, fold)
     return m

@@ -3,7 +3,12 @@
 
 The five RNAfold annotations (test_scoring.cc:52-55, 86-87, 152-154) and the
 macrostate / base-pair-probability thresholds (test_scoring.cc:83-259), for
-a parameter file (default: the shipped one) and a motif mode (default AUTO = 2: ADD in partition functions, REPLACE in the MFE).
+a parameter file (default: the shipped one) and a motif mode (default ADD = 0,
+the engine's default; 2 = AUTO: ADD in partition functions, REPLACE in the MFE),
+plus the 204 per-position ensemble classes of rhf(6) (test_scoring.cc:54-55,
+tests/pseudo_bracket.py).  The holo aptamer MFE annotation -9.22 is RNAfold's
+MFE under the REPLACE reading; it is reported for REPLACE and, as information,
+for the chosen mode.
 
 Usage: python tools/pin_report.py [params.par] [motif_mode]
 """
@@ -21,7 +26,7 @@ HAIRPIN = "ACGUGAAAACGU"
 
 def main():
     par = sys.argv[1] if len(sys.argv) > 1 else O.DEFAULT_PAR
-    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     P = O.Params(par)
     theo = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), mode)
     rhf = workloads.RHF6_SEQ.upper()
@@ -34,7 +39,9 @@ def main():
     ann("hairpin MFE " + s, e, -2.20)
     e, s = O.mfe(workloads.THEO_SEQ, params=P)
     ann("THEO apo MFE " + s, e, -6.20)
-    ann("THEO holo MFE", O.mfe_energy(workloads.THEO_SEQ, None, theo, params=P), -9.22)
+    theo_rep = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 1)
+    ann("THEO holo MFE (REPLACE)", O.mfe_energy(workloads.THEO_SEQ, None, theo_rep, params=P), -9.22)
+    info = [("THEO holo MFE (mode %d)" % mode, O.mfe_energy(workloads.THEO_SEQ, None, theo, params=P), -9.22)]
     ann("rhf(6) apo ensemble", O.pf_energy(rhf, params=P), -29.58)
     ann("rhf(6) holo ensemble", O.pf_energy(rhf, None, theo, params=P), -33.82)
 
@@ -101,7 +108,15 @@ def main():
         thr("rhf holo-only apo P%s" % ((i, j),), Ra[i, j], "<", ta)
         thr("rhf holo-only holo P%s" % ((i, j),), Rh[i, j], ">", th)
 
+    from tests.pseudo_bracket import APO_ANNOT, HOLO_ANNOT, position_probs, pseudo_bracket
+    for name, Rm, annot in (("apo", Ra, APO_ANNOT), ("holo", Rh, HOLO_ANNOT)):
+        pb = pseudo_bracket(position_probs(Rm))
+        for k, (got, want) in enumerate(zip(pb, annot)):
+            rows.append((got == want, "rhf %s ensemble class [%d]" % (name, k), got, want))
+
     bad = 0
+    for name, got, want in info:
+        print("info %-44s %-12.4f %.2f" % (name, got, want))
     for ok, name, got, want in rows:
         if not ok or "-v" in sys.argv:
             print("%-4s %-44s %-12s %s" % ("ok" if ok else "FAIL", name, got, want))
