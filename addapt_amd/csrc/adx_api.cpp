@@ -420,7 +420,7 @@ struct Problem {
     // base-pair probability terms: outside variants, requested pairs, per-walker results
     std::vector<int> bvars;
     std::vector<int> pairs;      // [n][3]: bvars index, i, j (1-based folded coordinates)
-    DevBuf<int> dBvars, dPairs;
+    DevBuf<int> dBvars, dPairs, dBvarSlot;
     DevBuf<double> dPairP;
     DevBuf<char> dScratch;       // outside tables in HBM when they do not fit LDS
     // MFE: packed 16-bit copies of the energy tables (kernels.hip MinPlus16)
@@ -481,6 +481,7 @@ struct Problem {
         ka.mode = mode;
         ka.bvars = dBvars.p;
         ka.n_bvars = static_cast<int>(bvars.size());
+        ka.bvar_slot = dBvarSlot.p;
         ka.pairs = dPairs.p;
         ka.n_pairs = static_cast<int>(pairs.size() / 3);
         ka.pair_p = dPairP.p;
@@ -608,6 +609,15 @@ struct Problem {
         }
         HIP_TRY(dGroups2.upload(groups2.data(), groups2.size(), stream));
         HIP_TRY(dBvars.upload(bvars.data(), bvars.size(), stream));
+        // every outside variant's position in the groups2 slot layout (the outside
+        // kernels read the proposal's inside tables there): an invariant, not a search
+        std::vector<int> bslot(bvars.size(), -1);
+        for (size_t b = 0; b < bvars.size(); b++)
+            for (size_t g = 0; g < groups2.size() && bslot[b] < 0; g++)
+                if (groups2[g] == bvars[b]) bslot[b] = static_cast<int>(g);
+        for (size_t b = 0; b < bslot.size(); b++)
+            if (bslot[b] < 0) return fail(ADX_EINVAL, "internal: outside variant %d has no fold group", bvars[b]);
+        HIP_TRY(dBvarSlot.upload(bslot.data(), bslot.size(), stream));
         HIP_TRY(dPairs.upload(pairs.data(), pairs.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
         s = upload_mfe16();
@@ -1267,12 +1277,11 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     c->last_ms = ms;
     double sk = 0.0, si = 0.0, so = 0.0;
     for (int k = 0; k < steps; k++) {
-        float e = 0.f, a = 0.f, b = 0.f;
+        float e = 0.f, b = 0.f;
         HIP_TRY(hipEventElapsedTime(&e, evs[4 * k], evs[4 * k + 3]));
-        HIP_TRY(hipEventElapsedTime(&a, evs[4 * k], evs[4 * k + 1]));
         HIP_TRY(hipEventElapsedTime(&b, evs[4 * k + 1], evs[4 * k + 2]));
         sk += e;
-        si += a;
+        si += e - b;   // the window minus its outside pass (kernels.hip launch_steps)
         so += b;
     }
     c->score_ms_total = sk;
@@ -1398,6 +1407,7 @@ extern "C" adx_status adx_bppm_batch(adx_ctx *c, int W, const char *seqs, int co
     KArgs ka = pb.kargs();
     ka.bvars = dbv.p;
     ka.n_bvars = 1;
+    ka.bvar_slot = nullptr;   // no stored tables are reused here
     ka.n_pairs = 0;
     ka.pairs = nullptr;
     ka.pair_p = nullptr;

@@ -153,6 +153,8 @@ struct KArgs {
     // base-pair probabilities (outside pass, bppm_kernel)
     const int *bvars;           // [n_bvars] variants folded with an outside pass
     int n_bvars;
+    const int *bvar_slot;       // [n_bvars] the variant's tables in the groups2 slot layout
+                                //   (2 * group + half; host-computed, adx_api.cpp upload_all)
     const int *pairs;           // [n_pairs][3]: bvars index, i, j (1-based, folded coordinates)
     int n_pairs;
     const double *pair_p;       // [W][n_pairs] probabilities written by bppm_kernel (score input)

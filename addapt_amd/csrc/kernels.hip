@@ -1649,13 +1649,8 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
     Inc inc{nullptr, nullptr, 0, 0};
     if (reuse && ka.tab) {
         const size_t B = 3 * size_t(ka.cells) + size_t(ka.Nmax) + 2;   // one variant's tables
-        size_t o = size_t(v) * B;                                      // score P = 1: group = variant
-        if (sp == 2) {
-            for (int g = 0; g < ka.n_groups2; g++) {
-                if (ka.groups2[2 * g] == v) { o = size_t(g) * 2 * B; break; }
-                if (ka.groups2[2 * g + 1] == v) { o = size_t(g) * 2 * B + B; break; }
-            }
-        }
+        // score P = 1: group = variant; P = 2: the groups2 position (host-computed)
+        const size_t o = (sp == 2 ? size_t(ka.bvar_slot[bv]) : size_t(v)) * B;
         const int cur = ka.cur_slot[w];
         inc.src = ka.tab + size_t(w) * 2 * ka.tab_slot + size_t(1 - cur) * ka.tab_slot + o;
         inc.m_lo = 4 * ka.Nmax + 8;   // no changed cell: every cell and q5 from src
@@ -2104,8 +2099,9 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
 }
 
-// evs (optional): 4 * nsteps events per step: window start, after the inside
-// folds, after the outside pass, window end (score written)
+// evs (optional): 4 * nsteps events per step: window start, outside pass
+// start, outside pass end, window end (score written); the inside share of a
+// window is the window minus its outside pass (adx_api.cpp)
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
     for (int s = 0; s < st.nsteps; s++) {
@@ -2138,16 +2134,15 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
                                st.prop_score, tv);
             e = hipGetLastError();
         } else {
+            // events 1 / 2 bracket the outside pass (here before the folds; none: empty)
+            if (evs) (void)hipEventRecord(evs[4 * s + 1], stream);
             if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
                 e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
                                 ka.bppm_scratch, stream);
                 if (e != hipSuccess) return e;
             }
+            if (evs) (void)hipEventRecord(evs[4 * s + 2], stream);
             e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
-            if (evs) {
-                (void)hipEventRecord(evs[4 * s + 1], stream);
-                (void)hipEventRecord(evs[4 * s + 2], stream);
-            }
         }
         if (evs) (void)hipEventRecord(evs[4 * s + 3], stream);
         if (e != hipSuccess) return e;

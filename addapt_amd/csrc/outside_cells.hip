@@ -400,13 +400,7 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
 
     // ---- the proposal's inside tables (score_kernel's P = sp_score layout, kernels.hip Inc)
     const size_t B = 3 * size_t(ka.cells) + size_t(ka.Nmax) + 2;
-    size_t go = size_t(v) * B;
-    if (sp_score == 2) {
-        for (int g = 0; g < ka.n_groups2; g++) {
-            if (ka.groups2[2 * g] == v) { go = size_t(g) * 2 * B; break; }
-            if (ka.groups2[2 * g + 1] == v) { go = size_t(g) * 2 * B + B; break; }
-        }
-    }
+    const size_t go = (sp_score == 2 ? size_t(ka.bvar_slot[bv]) : size_t(v)) * B;
     const int cur = ka.cur_slot[w];
     const float *src = ka.tab + size_t(w) * 2 * ka.tab_slot + size_t(1 - cur) * ka.tab_slot + go;
     const size_t Cs = size_t(ka.cells);   // the slot's table stride (Nmax cells)

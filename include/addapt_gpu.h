@@ -205,7 +205,8 @@ adx_status adx_last_kernel_ms(const adx_ctx *ctx, double *ms);
 adx_status adx_last_score_kernel_ms(const adx_ctx *ctx, double *avg_ms, int *launches);
 /* The same window split per launch (averages, ms): the inside folds (fold ->
  * energies or scores) and, when score terms read base-pair probabilities, the
- * outside pass on the stored inside tables (0 otherwise). */
+ * outside pass on the stored inside tables (0 otherwise); the inside share is
+ * the window minus its outside pass. */
 adx_status adx_last_kernel_split_ms(const adx_ctx *ctx, double *inside_ms, double *outside_ms);
 
 adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
