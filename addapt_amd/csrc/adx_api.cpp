@@ -25,6 +25,11 @@ size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
 hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
                         double *terms, float *dG, hipStream_t stream);
 hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream, hipEvent_t *evs);
+const char *inside_kernel_name(const KArgs &ka);
+size_t pf_ring_lds(const KArgs &ka);
+size_t outside_ring_lds(const KArgs &ka);
+size_t pf_ring_scratch_floats(const KArgs &ka, int W);
+const char *outside_kernel_name(const KArgs &ka);
 size_t bppm_lds_bytes(const KArgs &ka, bool *gout);
 size_t bppm_scratch_bytes(const KArgs &ka, int W);
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
@@ -423,6 +428,8 @@ struct Problem {
     DevBuf<int> dBvars, dPairs, dBvarSlot;
     DevBuf<double> dPairP;
     DevBuf<char> dScratch;       // outside tables in HBM when they do not fit LDS
+    bool pf_ring = false;        // PF folds by pf_ring_kernel (fixes the slot layout, kernels.hip)
+    DevBuf<float> dRingScr;      // its qb scratch for stateless launches
     // MFE: packed 16-bit copies of the energy tables (kernels.hip MinPlus16)
     DevBuf<DevTables> dT16;
     DevBuf<DevScaled> dX16;
@@ -497,6 +504,8 @@ struct Problem {
         ka.tab_valid = st ? dValid.p : nullptr;
         ka.chg = st ? dChg.p : nullptr;
         ka.gstep = dGstep.p;
+        ka.pf_ring = pf_ring ? 1 : 0;
+        ka.ring_scratch = dRingScr.p;
         return ka;
     }
 
@@ -620,6 +629,16 @@ struct Problem {
         HIP_TRY(dBvarSlot.upload(bslot.data(), bslot.size(), stream));
         HIP_TRY(dPairs.upload(pairs.data(), pairs.size(), stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        // PF folds longer than pf_cells covers take the ring kernel (pf_ring.hip).
+        // One choice per context: it fixes the layout of the walkers' stored
+        // tables, which every later kernel of the context must read the same way.
+        {
+            pf_ring = false;
+            const char *e = std::getenv("ADX_PF_KERNEL");
+            const bool rows = e && std::strcmp(e, "rows") == 0;
+            const KArgs k = kargs();
+            pf_ring = mode == 0 && !rows && pf_ring_lds(k) > 0 && (pairs.empty() || outside_ring_lds(k) > 0);
+        }
         s = upload_mfe16();
         if (s) return s;
         if (!pairs.empty() && bppm_lds_bytes(kargs(), nullptr) == 0)
@@ -651,6 +670,10 @@ struct Problem {
         if (so) return so;
         so = ensure_gstep(W);
         if (so) return so;
+        if (pf_ring) {   // qb scratch of the stateless ring folds
+            const size_t need = pf_ring_scratch_floats(kargs(), W);
+            if (dRingScr.n < need) HIP_TRY(dRingScr.alloc(need));
+        }
         if (!pairs.empty()) {
             adx_status s = ensure_pairs(W);
             if (s) return s;
@@ -880,6 +903,7 @@ struct adx_ctx {
     DevBuf<uint8_t> d_clo_par;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0.0;
+    std::string inside_kernel, outside_kernel;   // what the last adx_run_steps launched
     double score_ms_total = 0.0;   // sum of the score-kernel launch durations of the last run
     double inside_ms_total = 0.0, outside_ms_total = 0.0;   // the same windows split (inside, outside)
     int score_launches = 0;
@@ -1269,6 +1293,8 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     pb.state_on = true;   // incremental folds against the walkers' stored tables
     const KArgs ka_steps = pb.kargs();
     pb.state_on = false;
+    c->inside_kernel = inside_kernel_name(ka_steps);
+    c->outside_kernel = outside_kernel_name(ka_steps);
     HIP_TRY(launch_steps(ka_steps, pb.qbm, st, pb.stream, evs.data()));
     HIP_TRY(hipEventRecord(c->ev1, pb.stream));
     HIP_TRY(hipEventSynchronize(c->ev1));
@@ -1329,6 +1355,15 @@ extern "C" adx_status adx_last_kernel_split_ms(const adx_ctx *c, double *inside_
     const int n = c->score_launches;
     *inside_ms = n ? c->inside_ms_total / n : 0.0;
     *outside_ms = n ? c->outside_ms_total / n : 0.0;
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_last_kernel_names(const adx_ctx *c, char *inside, int inside_len, char *outside,
+                                            int outside_len) {
+    if (!c || !inside || !outside || inside_len <= 0 || outside_len <= 0)
+        return fail(ADX_EINVAL, "adx_last_kernel_names: bad argument");
+    std::snprintf(inside, size_t(inside_len), "%s", c->inside_kernel.c_str());
+    std::snprintf(outside, size_t(outside_len), "%s", c->outside_kernel.c_str());
     return ADX_OK;
 }
 

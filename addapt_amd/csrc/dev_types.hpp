@@ -173,6 +173,12 @@ struct KArgs {
     uint8_t *cur_slot;
     uint8_t *tab_valid;
     const int *chg;
+    // PF folds longer than pf_cells covers (pf_ring.hip): one workgroup per
+    // variant, qb in a ring of diagonals; the slot's qm / qm1 are then
+    // diagonal-major (decided once per context: every kernel reading the slot
+    // must agree).  ring_scratch: qb of stateless launches (W * 2 * n_groups2 * cells)
+    int pf_ring;
+    float *ring_scratch;
     // [W][n_variants] per-variant energies of the step's proposals when the score
     // waits for the outside pass (pair terms): score_kernel -> bppm_kernel
     // (re-using the inside tables just written) -> combine_kernel

@@ -1895,6 +1895,8 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 #endif
 #ifndef ADX_NT16
 #define ADX_NT16 512    // packed 16-bit MFE
+#define ADX_STR_(x) #x
+#define ADX_STR(x) ADX_STR_(x)
 #endif
 template <int P, int NT = (P == 2 ? ADX_NT2 : 512)>
 static size_t lds_size(const KArgs &ka, int pl, bool rt) {
@@ -1976,6 +1978,8 @@ __global__ void combine_kernel(KArgs ka, int W, const int *mask, double *scores,
 
 size_t mfe_cells_lds(const KArgs &ka);
 size_t pf_cells_lds(const KArgs &ka);
+hipError_t launch_pf_ring(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
+                          float *qscr, hipStream_t stream);
 hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
                            hipStream_t stream);
 hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
@@ -1995,16 +1999,53 @@ static bool pf_rows_forced() {
     return e && std::strcmp(e, "rows") == 0;
 }
 
-hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
-                          float *dG, const int *mask, hipStream_t stream) {
+// The fold kernel launch_score_m runs for a workload (one choice, used by the
+// dispatch and by the names the bench reports)
+enum class InsideK { MfeCells, MfeRows16, MinPlusP2, MinPlus512, PfCells, PfRing, SumProdP2, SumProd768, SumProd512 };
+static InsideK inside_choice(const KArgs &ka, bool has_g) {
     // ka.mode: 0 = partition functions (vrna_pf), 1 = minimum free energies
     if (ka.mode == 1 && ka.X16 && ka.ovf) {
+        KArgs k16 = ka;
+        k16.T = ka.T16;
+        k16.X = ka.X16;
+        return (!mfe_rows_forced() && mfe_cells_lds(k16) > 0) ? InsideK::MfeCells : InsideK::MfeRows16;
+    }
+    if (ka.mode == 1) return choose_p(ka) == 2 ? InsideK::MinPlusP2 : InsideK::MinPlus512;
+    if (ka.pf_ring) return InsideK::PfRing;   // the context's slot layout (adx_api.cpp upload_all)
+    if (has_g && !pf_rows_forced() && choose_p(ka) == 2 && ka.n_groups2 > 0 && pf_cells_lds(ka) > 0)
+        return InsideK::PfCells;
+    if (choose_p(ka) == 2) return InsideK::SumProdP2;
+    // one workgroup per CU (N = 150: the P = 1 tables take most of the LDS): 12
+    // waves instead of 8, 168 VGPRs a lane (16 waves at 128 spill: 29.9 vs 28.2 ms)
+    if (2 * lds_size<1, 512>(ka, 0, false) > size_t(LDS_LIMIT) - 2048) return InsideK::SumProd768;
+    return InsideK::SumProd512;
+}
+
+const char *inside_kernel_name(const KArgs &ka) {
+    switch (inside_choice(ka, ka.gstep != nullptr)) {
+        case InsideK::MfeCells: return "mfe_cells_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
+        case InsideK::MfeRows16: return "score_kernel<" ADX_STR(ADX_NT16) ", 1, MinPlus16> + score_kernel<MinPlus> (FP32 fallback launch)";
+        case InsideK::MinPlusP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, MinPlus>";
+        case InsideK::MinPlus512: return "score_kernel<512, 1, MinPlus>";
+        case InsideK::PfCells: return "pf_cells_kernel + combine_kernel";
+        case InsideK::PfRing: return "pf_ring_kernel + combine_kernel";
+        case InsideK::SumProdP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, SumProd>";
+        case InsideK::SumProd768: return "score_kernel<768, 1, SumProd>";
+        default: return "score_kernel<512, 1, SumProd>";
+    }
+}
+
+hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
+                          float *dG, const int *mask, hipStream_t stream) {
+    float *g = dG ? dG : ka.gstep;
+    const InsideK k = inside_choice(ka, g != nullptr);
+    if (k == InsideK::MfeCells || k == InsideK::MfeRows16) {
         // packed 16-bit folds (two variants per value, two workgroups per CU), then
         // the FP32 MinPlus kernel for the walkers whose values left the exact range
         KArgs k16 = ka;
         k16.T = ka.T16;
         k16.X = ka.X16;
-        hipError_t e = (!mfe_rows_forced() && mfe_cells_lds(k16) > 0)
+        hipError_t e = k == InsideK::MfeCells
                            ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
                            : launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         if (e != hipSuccess) return e;
@@ -2014,29 +2055,32 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
             return launch_score_t<ADX_NT2, 2, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
         return launch_score_t<512, 1, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
     }
-    if (ka.mode == 1) {
-        if (choose_p(ka) == 2)
-            return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
-        return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+    switch (k) {
+        case InsideK::MinPlusP2: return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+        case InsideK::MinPlus512: return launch_score_t<512, 1, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
+        case InsideK::PfCells: {
+            // lanes = cells (pf_cells.hip): energies to dG (or the gstep scratch), then the scores
+            hipError_t e = launch_pf_cells(ka, seqs, W, mask, g, stream);
+            if (e != hipSuccess) return e;
+            KArgs kc = ka;
+            kc.gstep = g;
+            hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
+            return hipGetLastError();
+        }
+        case InsideK::PfRing: {
+            // one workgroup per variant, qb ring (pf_ring.hip), then the scores
+            if (!g) return hipErrorInvalidValue;
+            hipError_t e = launch_pf_ring(ka, seqs, W, mask, g, ka.tab ? nullptr : ka.ring_scratch, stream);
+            if (e != hipSuccess) return e;
+            KArgs kc = ka;
+            kc.gstep = g;
+            hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
+            return hipGetLastError();
+        }
+        case InsideK::SumProdP2: return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
+        case InsideK::SumProd768: return launch_score_t<768, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
+        default: return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
     }
-    // partition functions: pf_cells_kernel (lanes = cells, pf_cells.hip) where it
-    // covers the length, energies to dG (or the gstep scratch), then the scores;
-    // else score_kernel<SumProd> (lanes = terms).  ADX_PF_KERNEL=rows forces the latter.
-    float *g = dG ? dG : ka.gstep;
-    if (g && !pf_rows_forced() && choose_p(ka) == 2 && ka.n_groups2 > 0 && pf_cells_lds(ka) > 0) {
-        hipError_t e = launch_pf_cells(ka, seqs, W, mask, g, stream);
-        if (e != hipSuccess) return e;
-        KArgs kc = ka;
-        kc.gstep = g;
-        hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
-        return hipGetLastError();
-    }
-    if (choose_p(ka) == 2) return launch_score_t<ADX_NT2, 2, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
-    // one workgroup per CU (N = 150: the P = 1 tables take most of the LDS): 12
-    // waves instead of 8, 168 VGPRs a lane (16 waves at 128 spill: 29.9 vs 28.2 ms)
-    if (2 * lds_size<1, 512>(ka, 0, false) > size_t(LDS_LIMIT) - 2048)
-        return launch_score_t<768, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
-    return launch_score_t<512, 1, SumProd>(ka, seqs, W, scores, terms, dG, mask, stream);
 }
 
 hipError_t launch_score(const KArgs &ka, bool, const uint8_t *seqs, int W, double *scores,
@@ -2093,6 +2137,32 @@ size_t outside_cells_lds(const KArgs &ka);
 hipError_t launch_outside_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *pair_p,
                                 int sp_score, hipStream_t stream);
 
+// The outside pass of an MC step with pair terms (launch_steps): the lanes =
+// cells kernel where it covers the workload, else bppm_kernel on the stored
+// tables (ADX_OUTSIDE_KERNEL=bppm forces the latter)
+size_t outside_ring_lds(const KArgs &ka);
+hipError_t launch_outside_ring(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *pair_p,
+                               hipStream_t stream);
+static bool outside_is_cells(const KArgs &ka) {
+    if (ka.pf_ring) return false;   // the ring's slot layout: outside_ring_kernel
+    const char *ok = std::getenv("ADX_OUTSIDE_KERNEL");
+    const bool old = ok && std::strcmp(ok, "bppm") == 0;
+    return !old && outside_cells_lds(ka) > 0;
+}
+const char *outside_kernel_name(const KArgs &ka) {
+    if (ka.n_pairs <= 0) return "";
+    if (!(ka.mode == 0 && ka.tab && ka.gstep)) {   // launch_steps' fallback branch: bppm from scratch
+        bool gout = false;
+        bppm_lds_bytes(ka, &gout);
+        return gout ? "bppm_kernel<1024, GOUT> (inside refold + outside)" : "bppm_kernel<512> (inside refold + outside)";
+    }
+    if (ka.pf_ring) return "outside_ring_kernel";
+    if (outside_is_cells(ka)) return "outside_cells_kernel";
+    bool gout = false;
+    bppm_lds_bytes(ka, &gout);
+    return gout ? "bppm_kernel<1024, GOUT>" : "bppm_kernel<512>";
+}
+
 // scratch: bppm_scratch_bytes(ka, W) bytes of device memory (null when 0)
 hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, double *full, int ld,
                        double *pair_p, char *scratch, hipStream_t stream) {
@@ -2121,9 +2191,9 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
             if (evs) (void)hipEventRecord(evs[4 * s + 1], stream);
             // lanes = cells outside kernel (outside_cells.hip) where it covers the
             // length, else bppm_kernel on the same stored tables
-            const char *ok = std::getenv("ADX_OUTSIDE_KERNEL");
-            const bool old = ok && std::strcmp(ok, "bppm") == 0;
-            e = (!old && outside_cells_lds(ka) > 0)
+            e = ka.pf_ring ? launch_outside_ring(ka, st.prop_seq, st.W, st.changed, const_cast<double *>(ka.pair_p),
+                                                 stream)
+                : outside_is_cells(ka)
                     ? launch_outside_cells(ka, st.prop_seq, st.W, st.changed, const_cast<double *>(ka.pair_p),
                                            choose_p(ka), stream)
                     : launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),

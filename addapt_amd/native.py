@@ -73,6 +73,7 @@ EXPORTS = [
     "adx_fold_pf", "adx_fold_mfe", "adx_fold_bpp", "adx_fold_free", "adx_ctx_create", "adx_ctx_destroy",
     "adx_ctx_info", "adx_walkers_init", "adx_run_steps", "adx_last_kernel_ms", "adx_last_score_kernel_ms",
     "adx_last_kernel_split_ms",
+    "adx_last_kernel_names",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
     "adx_walkers_import", "adx_set_temperature", "adx_bppm_batch",
 ]
@@ -108,6 +109,7 @@ def lib():
         L.adx_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         L.adx_last_score_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
         L.adx_last_kernel_split_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.adx_last_kernel_names.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
         L.adx_walkers_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_walkers_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_set_temperature.argtypes = [C.c_void_p, C.c_double]
@@ -356,6 +358,12 @@ class Engine:
         a, b = C.c_double(), C.c_double()
         _check(lib().adx_last_kernel_split_ms(self.ptr, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def last_kernel_names(self):
+        """(fold kernel(s), outside pass or "") the last run_steps launched."""
+        a, b = C.create_string_buffer(256), C.create_string_buffer(256)
+        _check(lib().adx_last_kernel_names(self.ptr, a, 256, b, 256))
+        return a.value.decode(), b.value.decode()
 
     def download(self):
         W = self.W

@@ -15,13 +15,21 @@ reference's own scoring path; config 3 without the bppm term).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--walkers 4096] [--length 100] [--fold mfe|pf]
 
+The default (MFE) line also carries `sub_records` measured in the same run:
+"pf" (the reference's own vrna_pf scoring path), "config3" (pf + bppm, N = 100)
+and "config4" (pf + bppm, N = 150, one GPU's shard), each with value,
+ms_per_step, the roofline of its dominant kernel (named from the engine's own
+dispatch, adx_last_kernel_names) and, for pf / config3, a CPU baseline.
+
 N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set) each
 process is one rank; a plain `python bench.py --gpus N` starts that launcher
 itself as a child process before anything touches the GPU (N larger than the
-visible GPU count is refused with exit status 2).  Walkers are sharded (weak
-scaling, global walker id = rank * W + w), no collective on the data path; a
-barrier + max-over-ranks brackets the timed region.  `--dry-run` replaces the
-engine by a host sleep over gloo (CPU-only test of the launch path).
+visible GPU count, read from the kfd topology, is refused with exit status 2).
+Walkers are sharded (weak scaling, global walker id = rank * W + w), no
+collective on the data path; a barrier + max-over-ranks brackets the timed
+region.  `--dist-backend gloo --share-device` rehearses the N-rank paths
+(sharding, replica exchange) on one GPU; `--dry-run` replaces the engine by a
+host sleep over gloo (CPU-only test of the launch path).
 """
 import argparse
 import json
@@ -60,6 +68,15 @@ def parse():
                          "(default profiles/traffic_latest_<fold>.json)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks, a host sleep per step (tests the --gpus N launch path)")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1: nccl (= RCCL, one GPU per rank) or gloo (rehearsal on host tensors)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="N > 1 rehearsal on one GPU: every rank runs its engine on device 0 "
+                         "(use with --dist-backend gloo)")
+    ap.add_argument("--no-sub-records", action="store_true",
+                    help="skip the PF / config 3 / config 4 sub-records of the default (MFE) run")
+    ap.add_argument("--sub-steps-c4", type=int, default=60,
+                    help="timed steps of the config-4 sub-record (N = 150)")
     return ap.parse_args()
 
 
@@ -73,14 +90,13 @@ def _free_port():
 
 def spawn_ranks(a):
     """`bench.py --gpus N` without a launcher: start torch.distributed.run as a
-    child (nothing here has touched the GPU: device_count() does not initialise
-    it) and return its exit status."""
+    child and return its exit status.  Nothing here touches the GPU: the
+    visible GPUs are counted from the kfd topology (gpu_count); each rank
+    checks its own device again after the launch."""
     import subprocess
 
-    if not a.dry_run:
-        import torch
-
-        visible = torch.cuda.device_count()
+    if not a.dry_run and not a.share_device:
+        visible = gpu_count()
         if a.gpus > visible:
             print("bench.py: --gpus %d but %d GPU(s) visible" % (a.gpus, visible), file=sys.stderr)
             return 2
@@ -145,29 +161,6 @@ def cpu_baseline(tmpl, active, walker_seqs, budget_s, fold, terms):
             "reference_2016_per_core": 14.4}
 
 
-def pf_kernel_label(bppm, length=100):
-    """The PF kernels of one step's score window (kernels.hip launch_score_m / launch_steps):
-    pf_cells_kernel up to N = 100 (pf_cells.hip PX_NMAX), outside_cells_kernel up to
-    N = 112 (outside_cells.hip OX_NMAX), the general kernels beyond (their LDS)."""
-    inside = ("score_kernel<SumProd> (lanes = terms)"
-              if os.environ.get("ADX_PF_KERNEL") == "rows" or length > 100
-              else "pf_cells_kernel (lanes = cells)")
-    if bppm:
-        return inside + " + %s + combine_kernel (one event window per step)" % outside_kernel(length)
-    return inside + " + combine_kernel"
-
-
-def outside_kernel(length):
-    return "outside_cells_kernel" if length <= 112 else "bppm_kernel<512, GOUT>"
-
-
-def mfe_kernel_label():
-    """The MFE fold kernel the engine launches (kernels.hip mfe_kernel_choice)."""
-    k = os.environ.get("ADX_MFE_KERNEL", "cells")
-    return {"rows": "score_kernel<MinPlus16> (lanes = terms)"}.get(
-        k, "mfe_cells_kernel (lanes = cells, 2 folds per cell)") + " + FP32 MinPlus fallback launch"
-
-
 def dry_run(a, rank, world):
     """CPU-only rehearsal of the rank launch: gloo barrier, a sleep per step, max over ranks."""
     import torch.distributed as dist
@@ -192,6 +185,188 @@ def dry_run(a, rank, world):
         dist.destroy_process_group()
 
 
+def _traffic(a_traffic_json, fold, bppm, length, outside_name):
+    """PMC bytes per launch of the dominant kernel from the summary of this exact
+    workload (tools/pmc_traffic.py), or (None, None)."""
+    path = a_traffic_json or os.path.join(ROOT, "profiles", "traffic_latest_%s%s%s.json" % (
+        fold, "_bppm" if bppm else "", "" if length == 100 else "_n%d" % length))
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        tj = json.load(f)
+    traffic = tj.get("bytes_per_launch")
+    if bppm:   # the outside pass's own bytes (the summary holds every kernel of the window)
+        key = outside_name.split("<")[0].split(" ")[0]
+        own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if key and key in name]
+        traffic = own[0] if own else None
+    return traffic, os.path.relpath(path, ROOT)
+
+
+def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, dev, local_rank,
+            traffic_json=None, cpu=False, cpu_seconds=15.0):
+    """Run one workload (W walkers of this rank) and return its record: value
+    (all ranks), ms_per_step, roofline of the dominant kernel, outcomes."""
+    from addapt_amd import native, roofline, shard, workloads
+
+    tmpl, active = workloads.synthetic(length)
+    terms = workloads.config_objective(length, bppm=bppm)
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    replica_mode = a.replica_interval > 0 and world > 1
+    if replica_mode:
+        from addapt_amd import replica
+
+        temps = replica.ladder_temperatures(world)
+        th = native.make_thermostat("fixed", t=temps[rank])
+    else:
+        th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank, fold_mode=fold)
+    W = a.walkers
+    seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + gids_rank[0])
+    eng.walkers_init(gids_rank, seqs)
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    if warmup > 0:
+        eng.run_steps(warmup)
+    _, _, c0 = eng.download()
+    barrier()
+    t0 = time.perf_counter()
+    rx = None
+    if replica_mode:
+        rx = replica.run(eng, dist, rank, world, steps, a.replica_interval, temps, seed=0, device="cuda")
+    else:
+        eng.run_steps(steps)
+    barrier()
+    t1 = time.perf_counter()
+    kernel_ms = eng.last_kernel_ms()            # whole timed run_steps (3 kernels per step)
+    score_ms, launches = eng.last_score_kernel_ms()   # the step's score window, per launch
+    inside_ms, outside_ms = eng.last_kernel_split_ms()   # the same window split per kernel
+    inside_name, outside_name = eng.last_kernel_names()  # what the engine launched
+    _, _, c1 = eng.download()
+    elapsed = shard.max_over_ranks(t1 - t0, dist, device=dev)
+    value = W * steps * world / elapsed
+
+    # algorithmic work of the launch: scored steps x the folds' (+ outside passes') terms
+    dc = c1 - c0
+    scored = int(dc[:, 0].sum() + dc[:, 1].sum() + dc[:, 3].sum())
+    outcomes = shard.sum_over_ranks(dc.sum(axis=0), dist, device=dev)
+    sample = [tmpl] + seqs[:7]
+    work = roofline.pf_flops if fold == "pf" else roofline.mfe_ops
+    f_free = sum(work(x, None) for x in sample) / len(sample)
+    f_act = sum(work(x, active) for x in sample) / len(sample)
+    flop_inside = 2 * f_free + 2 * f_act           # apo/holo x free/active
+    flop_per_scored = flop_inside
+    f_out = 0.0
+    if bppm:   # outside passes of the apo and holo unconstrained folds (on the stored inside tables)
+        f_out = 2 * sum(roofline.outside_flops(x, None) for x in sample) / len(sample)
+        flop_per_scored += f_out
+    scored_pl = scored / max(1, steps)                             # scored walkers per launch
+    launch_flops = scored_pl * flop_per_scored                     # per score window (one per step)
+    # the dominant kernel's own time: the outside pass with pair terms, else the
+    # window (inside folds + the score combine)
+    kern_ms, kern_flops = (outside_ms, scored_pl * f_out) if bppm else (score_ms, launch_flops)
+    achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
+    # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
+    # groups x value arrays (MFE: one packed apo/holo array; PF: two) x
+    # (3 cell tables + q5) x 4 B
+    cells = (length - 4) * (length - 3) // 2
+    state_bytes = 2 * (1 if fold == "mfe" else 2) * (3 * cells + length + 2) * 4
+    traffic, traffic_src = _traffic(traffic_json, fold, bppm, length, outside_name)
+    peak, peak_note = roofline.valu_peak(fold)
+    roof = {
+        "bound": "valu",
+        "achieved": achieved,
+        "peak": peak,
+        "unit": "TFLOP/s" if fold == "pf" else "Top/s",
+        "frac": (achieved / peak) if achieved else None,
+        "traffic": traffic,
+        "compute_unit": peak_note,
+        "kernel": (outside_name + " (events around its launch; the window also holds " + inside_name + ")")
+                  if bppm else inside_name,
+        "inside_kernel": inside_name,
+        "outside_kernel": outside_name or None,
+        "traffic_source": traffic_src,
+        "kernel_ms_per_launch": kern_ms,
+        "window_ms_per_launch": score_ms,
+        "inside_ms_per_launch": inside_ms,
+        "outside_ms_per_launch": outside_ms if bppm else None,
+        "inside_frac": ((scored_pl * flop_inside / (inside_ms * 1e-3) / 1e12) / peak
+                        if bppm and inside_ms > 0 else None),
+        "launches": launches,
+        "all_kernels_ms_per_step": kernel_ms / steps,
+        "flop_per_scored_step": flop_per_scored,
+        "flop_per_launch": launch_flops,
+        "scored_walkers_per_launch": scored_pl,
+        # HBM bytes of one launch by design: each scored walker reads its proposal
+        # (N B), writes its score (8 B), and writes its fold tables for the next
+        # incremental refold (read back for the unchanged cells, <= the same again)
+        "algorithmic_bytes_per_launch": scored_pl * (length + 8 + 2 * state_bytes),
+        "state_bytes_per_scored_walker": state_bytes,
+        "hbm_peak_GBps": HBM_PEAK_GBPS,
+    }
+    rec = {
+        "value": value,
+        "unit": "MC steps/s",
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "dtype": "i16x2" if fold == "mfe" else "fp32",
+        "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
+                    "0.32 uM)%s, 4 %s%s per scored step, synthetic %d-nt sgRNA template "
+                    "(SURVEY.md 8d), %d walkers per GPU, %s"
+                    % ("BASELINE configs[1] (MFE-fold score only)" if fold == "mfe"
+                       else ("BASELINE config %d (pf + bppm score)" % (3 if length == 100 else 4)) if bppm
+                       else "partition-function score (config 3 without bppm)",
+                       " + apo 'not pair(0,N-1)' / holo 'pair(0,N-1)'" if bppm else "",
+                       "minimum-free-energy folds" if fold == "mfe" else "McCaskill inside PFs",
+                       " + 2 inside/outside (bppm) passes" if bppm else "",
+                       length, W,
+                       "replica ladder T_r = 0.5*1.5^r" if replica_mode else "annealing 5 to 0 in 300 steps"),
+        "fold": fold,
+        "bppm": bppm,
+        "length": length,
+        "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, outcomes)},
+        "roofline": roof,
+    }
+    if rx is not None:
+        att = shard.sum_over_ranks([rx["attempted"], rx["accepted"], rx["rounds"]], dist, device=dev)
+        rec["exchange"] = {"rounds_per_rank": rx["rounds"], "attempted": att[0], "accepted": att[1],
+                           "interval": a.replica_interval, "temperatures": temps}
+    if cpu and rank == 0 and world == 1:
+        rec["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, cpu_seconds, fold, terms)
+    del eng
+    return rec
+
+
+def gpu_count():
+    """Visible GPUs without touching HIP (the launcher starts before any GPU call):
+    the kfd topology's GPU nodes, narrowed by *_VISIBLE_DEVICES."""
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in os.listdir(base):
+            try:
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if n else len(ids)
+    return n
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -205,172 +380,84 @@ def main():
     if a.dry_run:
         return dry_run(a, rank, world)
     dist = None
+    dev = None
+    device = 0 if a.share_device else local_rank
     if world > 1:
         import torch
         import torch.distributed as dist_
 
-        torch.cuda.set_device(local_rank)
-        dist_.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if not a.share_device and local_rank >= torch.cuda.device_count():
+            print("bench.py: rank %d has no GPU (%d visible)" % (local_rank, torch.cuda.device_count()),
+                  file=sys.stderr)
+            sys.exit(2)
+        torch.cuda.set_device(device)
+        if a.dist_backend == "nccl":
+            dist_.init_process_group("nccl", device_id=torch.device("cuda", device))
+            dev = "cuda"
+        else:   # rehearsal: gloo on host tensors (ranks may share one GPU)
+            dist_.init_process_group("gloo")
         dist = dist_
 
-    from addapt_amd import native, roofline, shard, workloads
+    from addapt_amd import shard
 
     if a.bppm:
         a.fold = "pf"
-    tmpl, active = workloads.synthetic(a.length)
-    terms = workloads.config_objective(a.length, bppm=a.bppm)
-    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
-    replica_mode = a.replica_interval > 0 and world > 1
-    if replica_mode:
-        from addapt_amd import replica
-
-        temps = replica.ladder_temperatures(world)
-        th = native.make_thermostat("fixed", t=temps[rank])
-    else:
-        th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
-    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th, device=local_rank,
-                        fold_mode=a.fold)
     W = a.walkers
     gids = shard.walker_ids(rank, world, W)
-    seqs = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + gids[0])
-    eng.walkers_init(gids, seqs)
-
-    def barrier():
-        if dist is not None:
-            import torch
-
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    if a.warmup > 0:
-        eng.run_steps(a.warmup)
-    _, _, c0 = eng.download()
-    barrier()
-    t0 = time.perf_counter()
-    if replica_mode:
-        rx = replica.run(eng, dist, rank, world, a.steps, a.replica_interval, temps, seed=0,
-                         device="cuda")
-    else:
-        eng.run_steps(a.steps)
-    barrier()
-    t1 = time.perf_counter()
-    kernel_ms = eng.last_kernel_ms()            # whole timed run_steps (3 kernels per step)
-    score_ms, launches = eng.last_score_kernel_ms()   # the step's score window, per launch
-    inside_ms, outside_ms = eng.last_kernel_split_ms()   # the same window split per kernel
-    _, _, c1 = eng.download()
-    elapsed = shard.max_over_ranks(t1 - t0, dist, device="cuda" if dist is not None else None)
-    steps_total = W * a.steps * world
-    value = steps_total / elapsed
-
-    # algorithmic FLOPs of the launch: scored steps x sum over the PF variants
-    dc = c1 - c0
-    scored = int(dc[:, 0].sum() + dc[:, 1].sum() + dc[:, 3].sum())
-    outcomes = shard.sum_over_ranks(dc.sum(axis=0), dist, device="cuda" if dist is not None else None)
-    sample = [tmpl] + seqs[:7]
-    work = roofline.pf_flops if a.fold == "pf" else roofline.mfe_ops
-    f_free = sum(work(s, None) for s in sample) / len(sample)
-    f_act = sum(work(s, active) for s in sample) / len(sample)
-    flop_inside = 2 * f_free + 2 * f_act           # apo/holo x free/active
-    flop_per_scored = flop_inside
-    f_out = 0.0
-    if a.bppm:   # outside passes of the apo and holo unconstrained folds (on the stored inside tables)
-        f_out = 2 * sum(roofline.outside_flops(s, None) for s in sample) / len(sample)
-        flop_per_scored += f_out
-    scored_pl = scored / max(1, a.steps)                             # scored walkers per launch
-    launch_flops = scored_pl * flop_per_scored                      # per score window (one per step)
-    # the dominant kernel's own time: the outside pass with --bppm, else the window
-    # (inside folds + the score combine)
-    kern_ms, kern_flops = (outside_ms, scored_pl * f_out) if a.bppm else (score_ms, launch_flops)
-    achieved_tflops = kern_flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
-    # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
-    # groups x value arrays (MFE: one packed apo/holo array; PF: two) x
-    # (3 cell tables + q5) x 4 B
-    cells = (a.length - 4) * (a.length - 3) // 2
-    state_bytes = 2 * (1 if a.fold == "mfe" else 2) * (3 * cells + a.length + 2) * 4
-    traffic, traffic_src = None, None
-    if a.traffic_json is None:
-        # the PMC summary of this exact workload (fold, pair terms, length), else null
-        a.traffic_json = os.path.join(ROOT, "profiles", "traffic_latest_%s%s%s.json" % (
-            a.fold, "_bppm" if a.bppm else "", "" if a.length == 100 else "_n%d" % a.length))
-    if a.traffic_json and os.path.exists(a.traffic_json):
-        with open(a.traffic_json) as f:
-            tj = json.load(f)
-        traffic = tj.get("bytes_per_launch")
-        if a.bppm:   # the dominant kernel's own bytes (the summary holds every kernel of the window)
-            own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if outside_kernel(a.length).split("<")[0] in name]
-            traffic = own[0] if own else None
-        traffic_src = os.path.relpath(a.traffic_json, ROOT)
-    peak, peak_note = roofline.valu_peak(a.fold)
-    roof = {
-        "bound": "valu",
-        "achieved": achieved_tflops,
-        "peak": peak,
-        "unit": "TFLOP/s" if a.fold == "pf" else "Top/s",
-        "frac": (achieved_tflops / peak) if achieved_tflops else None,
-        "traffic": traffic,
-        "compute_unit": peak_note,
-        "kernel": (outside_kernel(a.length) + " (events around its launch; the window also holds "
-                   + pf_kernel_label(False, a.length) + ")") if a.bppm
-                  else mfe_kernel_label() if a.fold == "mfe" else pf_kernel_label(False, a.length),
-        "traffic_source": traffic_src,
-        "kernel_ms_per_launch": kern_ms,
-        "window_ms_per_launch": score_ms,
-        "inside_ms_per_launch": inside_ms,
-        "outside_ms_per_launch": outside_ms if a.bppm else None,
-        "inside_frac": ((scored_pl * flop_inside / (inside_ms * 1e-3) / 1e12) / peak
-                        if a.bppm and inside_ms > 0 else None),
-        "launches": launches,
-        "all_kernels_ms_per_step": kernel_ms / a.steps,
-        "flop_per_scored_step": flop_per_scored,
-        "flop_per_launch": launch_flops,
-        "scored_walkers_per_launch": scored / max(1, a.steps),
-        # HBM bytes of one launch by design: each scored walker reads its proposal
-        # (N B), writes its score (8 B), and writes its fold tables for the next
-        # incremental refold (read back for the unchanged cells, <= the same again)
-        "algorithmic_bytes_per_launch": (scored / max(1, a.steps)) * (a.length + 8 + 2 * state_bytes),
-        "state_bytes_per_scored_walker": state_bytes,
-        "hbm_peak_GBps": HBM_PEAK_GBPS,
-    }
+    rec = measure(a, a.fold, a.bppm, a.length, a.steps, a.warmup, rank, world, gids, dist, dev, device,
+                  traffic_json=a.traffic_json, cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds)
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": rec["value"],
         "unit": "MC steps/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": elapsed / a.steps * 1e3,
+        "ms_per_step": rec["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         # MFE: integer dcal/mol, apo|holo as two int16 halves of one 32-bit word
         # (v_pk_add_i16 / v_pk_min_i16); PF: fp32 Boltzmann factors
-        "dtype": "i16x2" if a.fold == "mfe" else "fp32",
+        "dtype": rec["dtype"],
         "data": "synthetic",
         "config": {
-            "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
-                        "0.32 uM)%s, 4 %s%s per scored step, synthetic %d-nt sgRNA template "
-                        "(SURVEY.md 8d), %d walkers per GPU, annealing 5 to 0 in 300 steps"
-                        % ("BASELINE configs[1] (MFE-fold score only)" if a.fold == "mfe"
-                           else ("BASELINE config 3/4 (pf + bppm score)" if a.bppm
-                                 else "partition-function score (config 3 without bppm)"),
-                           " + apo 'not pair(0,N-1)' / holo 'pair(0,N-1)'" if a.bppm else "",
-                           "minimum-free-energy folds" if a.fold == "mfe" else "McCaskill inside PFs",
-                           " + 2 inside/outside (bppm) passes" if a.bppm else "",
-                           a.length, W),
+            "workload": rec["workload"],
             "fold": a.fold,
             "bppm": a.bppm,
             "walkers_per_gpu": W,
             "global_walkers": W * world,
             "length": a.length,
-            "parallelism": ("replica exchange x%d (RCCL neighbour swap every %d steps)"
-                            % (world, a.replica_interval)) if replica_mode
+            "parallelism": ("replica exchange x%d (%s neighbour swap every %d steps)"
+                            % (world, "RCCL" if a.dist_backend == "nccl" else "gloo", a.replica_interval))
+            if a.replica_interval > 0 and world > 1
             else "walker-sharded x%d (no data-path collective)" % world,
-            "outcomes": {k: int(v) for k, v in zip(native.OUTCOMES, outcomes)},
+            "dist_backend": a.dist_backend if world > 1 else None,
+            "shared_device": bool(a.share_device and world > 1),
+            "outcomes": rec["outcomes"],
         },
-        "roofline": roof,
+        "roofline": rec["roofline"],
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(tmpl, active, seqs, a.cpu_seconds, a.fold, terms)
+    if "exchange" in rec:
+        out["exchange"] = rec["exchange"]
+    if "cpu_baseline" in rec:
+        out["cpu_baseline"] = rec["cpu_baseline"]
+    # the reference's own scoring path (vrna_pf, scoring.cc:53-71) measured in the
+    # same run: PF, config 3 (pf + bppm, N = 100) and config 4's per-GPU shard
+    # (pf + bppm, N = 150), each with its dominant kernel's roofline
+    if not a.no_sub_records and a.fold == "mfe" and not a.bppm and a.replica_interval == 0:
+        subs = {}
+        for name, fold, bppm, length, steps, cpu in (
+                ("pf", "pf", False, 100, a.steps, True),
+                ("config3", "pf", True, 100, a.steps, True),
+                ("config4", "pf", True, 150, min(a.steps, a.sub_steps_c4), False)):
+            r = measure(a, fold, bppm, length, steps, min(a.warmup, 5), rank, world, gids, dist, dev, device,
+                        cpu=cpu and not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds * 2.0 / 3.0)
+            subs[name] = {k: r[k] for k in ("value", "unit", "steps", "ms_per_step", "dtype", "workload",
+                                            "outcomes", "roofline") if k in r}
+            if "cpu_baseline" in r:
+                subs[name]["cpu_baseline"] = r["cpu_baseline"]
+        out["sub_records"] = subs
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

@@ -208,6 +208,9 @@ adx_status adx_last_score_kernel_ms(const adx_ctx *ctx, double *avg_ms, int *lau
  * outside pass on the stored inside tables (0 otherwise); the inside share is
  * the window minus its outside pass. */
 adx_status adx_last_kernel_split_ms(const adx_ctx *ctx, double *inside_ms, double *outside_ms);
+/* Names of the fold kernel(s) and of the outside pass ("" without pair terms)
+ * the last adx_run_steps launched, from the engine's own dispatch choice. */
+adx_status adx_last_kernel_names(const adx_ctx *ctx, char *inside, int inside_len, char *outside, int outside_len);
 
 adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
 

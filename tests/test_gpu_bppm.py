@@ -144,12 +144,13 @@ def test_mc_trajectory_with_pair_terms(native, oracle):
         assert list(counters[w]) == ref["counters"]
 
 
-@pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (110, False), (150, False)])
+@pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (110, False), (150, False),
+                                           (150, True)])
 def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
     """Configs 3 / 4 shape: inside folds first (N <= 100: pf_cells_kernel,
-    else score_kernel), the outside pass on the proposal's stored inside tables
-    (N <= 112: outside_cells_kernel, lanes = cells; N = 150: bppm_kernel with
-    global scratch), then the scores.  Every
+    else pf_ring_kernel), the outside pass on the proposal's stored inside tables
+    (N <= 100: outside_cells_kernel; N > 100: outside_ring_kernel on the ring
+    kernel's diagonal-major slot), then the scores.  Every
     scored proposal's score matches the oracle's from-scratch score of that
     proposal (ln p terms within 2e-3).  motif_pairs: pair terms inside the
     ligand motif (credited from the motif's closing cell in the holo fold)."""
@@ -185,9 +186,9 @@ def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
 @pytest.mark.parametrize("N", [100, 150])
 def test_mc_pair_terms_full_size(native, oracle, N):
     """Configs 3 / 4 at their per-GPU size (4096 walkers; N = 100: pf_cells +
-    outside_cells, N = 150: the 16-wave score_kernel + bppm_kernel): counters sum
-    to the steps, and sampled walkers' final scores (pair probabilities
-    included) equal the oracle's from-scratch scores of their final sequences."""
+    outside_cells, N = 150: pf_ring + outside_ring): counters sum to the steps,
+    and sampled walkers' final scores (pair probabilities included) equal the
+    oracle's from-scratch scores of their final sequences."""
     tmpl, active = workloads.synthetic(N)
     terms = _objective(N)
     th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
@@ -198,6 +199,9 @@ def test_mc_pair_terms_full_size(native, oracle, N):
     eng.run_steps(2)
     final, scores, counters = eng.download()
     assert (counters.sum(axis=1) == 2).all()
+    inside, outside = eng.last_kernel_names()
+    assert (inside.startswith("pf_cells_kernel") and outside == "outside_cells_kernel") if N <= 100 else \
+        (inside.startswith("pf_ring_kernel") and outside == "outside_ring_kernel"), (inside, outside)
     sf = _oracle_sf(oracle, terms)
     for w in list(range(0, W, 683)) + [W - 1]:
         ref, _ = sf.score(final[w], [active])

@@ -1,0 +1,151 @@
+"""GPU parity of pf_ring_kernel (pf_ring.hip): partition functions of folds
+longer than pf_cells_kernel covers (101 <= N <= 150; BASELINE config 4's
+N = 150), one workgroup per variant with qb in a ring of diagonals and the
+exterior sums read back from the walker's table slot.
+
+Bar (north_star): fold free energies within 1e-4 kcal/mol of the FP64 oracle,
+MC trajectories (positions, bases, outcomes, counters) identical, incremental
+refolds bit-identical to from-scratch folds."""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from addapt_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+DG_TOL = 1e-4
+
+
+def rand_seq(rng, n):
+    return "".join(rng.choice("ACGU") for _ in range(n))
+
+
+def rand_constraint(rng, n, p_x=0.1, n_pairs=2):
+    c = ["."] * n
+    for _ in range(n_pairs):
+        i = rng.randrange(0, n - 8)
+        j = rng.randrange(i + 5, n)
+        if all(ch == "." for ch in c[i:j + 1]):
+            c[i], c[j] = "(", ")"
+    for k in range(n):
+        if c[k] == "." and rng.random() < p_x:
+            c[k] = rng.choice("x|<>") if rng.random() < 0.2 else "x"
+    return "".join(c)
+
+
+def _motif(oracle):
+    return oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
+
+
+def test_ring_fold_layer(native, oracle):
+    """Single folds (adx_fold_pf: stateless, qb scratch) at ring lengths, with
+    random hard constraints and the ligand motif."""
+    rng = random.Random(101)
+    apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
+    e = oracle.theo_bonus()
+    for n in (101, 117, 128, 150):
+        for _ in range(2):
+            s = rand_seq(rng, n)
+            for cst in (None, rand_constraint(rng, n)):
+                f = native.Fold(s)
+                if cst:
+                    f.add_constraint(cst)
+                g = f.pf()
+                ref = np.float32(oracle.pf_energy(s, cst))
+                if math.isinf(ref):
+                    assert math.isinf(g) and g > 0, (n, cst, g)
+                else:
+                    assert abs(g - ref) <= DG_TOL, (n, s, cst, g, float(ref))
+        s = rand_seq(rng, (n - 27) // 2) + apt
+        s = s + rand_seq(rng, n - len(s))
+        f = native.Fold(s)
+        f.add_motif(apt, fold, e)
+        g = f.pf()
+        ref = oracle.pf_energy(s, None, oracle.make_motif(apt, fold, e))
+        assert abs(g - np.float32(ref)) <= DG_TOL, (n, g, ref)
+
+
+@pytest.mark.parametrize("N", [101, 150])
+def test_ring_score_batch(native, oracle, N):
+    tmpl, active = workloads.synthetic(N)
+    terms = workloads.default_objective()
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt)
+    seqs = workloads.walker_sequences(tmpl, [active], 12)
+    sc, tv, dg = eng.score_batch(seqs)
+    m = _motif(oracle)
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(0, 12, 4):
+            ref = oracle.pf_energy(seqs[w], active if mac >= 0 else None, m if cond == 1 else None)
+            assert abs(dg[w, v] - np.float32(ref)) <= DG_TOL, (N, v, w, dg[w, v], ref)
+    sf = oracle.ScoreFunction(terms, aptamer=m)
+    for w in range(12):
+        ref, tref = sf.score(seqs[w], [active])
+        assert abs(sc[w] - ref) <= 2e-3, (w, sc[w], ref)
+
+
+def _replay(native, oracle, N, seeds, steps, contexts=None, macro_extra=None):
+    tmpl, active = workloads.synthetic(N)
+    macro = [active] + ([macro_extra] if macro_extra else [])
+    terms = workloads.default_objective() + ([("apo", 1, True, 2.0)] if macro_extra else [])
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    eng = native.Engine(tmpl, macro, terms, aptamer=apt, contexts=contexts, thermostat=th)
+    seqs = workloads.walker_sequences(tmpl, macro, len(seeds))
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = oracle.ScoreFunction(terms, aptamer=_motif(oracle), contexts=contexts)
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=30)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], macro, therm_o, seed, steps, forced=forced, tie_eps=1e-6)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert tr["base"][w::len(seeds)] == ref["base"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                a, b = tr["proposed_score"][s, w], ref["proposed_score"][s]
+                assert abs(a - b) <= 2e-3, (N, w, s, a, b)
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert abs(scores[w] - ref["score"]) <= 2e-3
+        assert list(counters[w]) == ref["counters"]
+
+
+def test_ring_trajectory_n150(native, oracle):
+    """Incremental refolds at config 4's length against the oracle's full folds."""
+    _replay(native, oracle, 150, [31, 32, 33, 34], 25)
+
+
+def test_ring_trajectory_contexts(native, oracle):
+    """Contexts push the folded length into the ring range (96 + up to 9 nt) and
+    shift the changed positions; a second macrostate adds a constrained group."""
+    ctx = [("GGACA", "UUAC"), ("", "CCCAGU"), ("AUAUAUA", "")]
+    N = 96
+    other = "." * 8 + "(" + "." * 16 + ")" + "." * (N - 26)   # mutable positions (the aptamer is frozen)
+    _replay(native, oracle, N, [41, 42, 43], 20, contexts=ctx, macro_extra=other)
+
+
+def test_ring_incremental_consistency(native):
+    """512 walkers x 40 steps at N = 150: every stored score equals a
+    from-scratch score of the final sequence bit for bit."""
+    tmpl, active = workloads.synthetic(150)
+    terms = workloads.default_objective()
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300)
+    eng = native.Engine(tmpl, [active], terms, aptamer=apt, thermostat=th)
+    W = 512
+    seqs = workloads.walker_sequences(tmpl, [active], W)
+    eng.walkers_init(list(range(W)), seqs)
+    eng.run_steps(40)
+    final, scores, counters = eng.download()
+    assert (counters.sum(axis=1) == 40).all()
+    assert "pf_ring_kernel" in eng.last_kernel_names()[0]
+    sc, _, _ = eng.score_batch(final)
+    bad = np.nonzero(scores != sc)[0]
+    assert bad.size == 0, [(int(w), scores[w], sc[w]) for w in bad[:8]]
