@@ -25,12 +25,34 @@
 
 #include "dev_types.hpp"
 #include "fold_common.hpp"
+
+namespace adx {
+#ifdef ADX_STAMP
+// Diagnostic build only: per-wave cycle sums of the phases (s_memtime), read
+// back through adx_debug_stamps_outside_ring().  Never in the product.
+__device__ unsigned long long g_stamps_or[16][8];
+#define OSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#endif
+}  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps_outside_ring(unsigned long long *out, int reset) {  // [16][8]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_or), sizeof(adx::g_stamps_or)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_or), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif
+
 #include "outside_common.hpp"
 
 namespace adx {
 namespace {
 
 constexpr int OR_SETS = 3;
+constexpr int OR_NB = 8;              // interior-loop waves 0-7 (records on 7); multiloop sums on 8-15
 constexpr int OR_NMIN = 101, OR_NMAX = 190;
 constexpr int OR_SLACK = 64;
 
@@ -47,7 +69,7 @@ struct OrLay {
         QW = o;   o += a16(size_t(OX_WIN) * RL * 4);             // qbb * mismatchI(outer) window
         OW = o;   o += a16(size_t(OX_WIN) * RL);                 // outer codes window
         PART = o; o += a16(size_t(2) * OR_SETS * OX_NB * WAVE * 4);
-        MLP = o;  o += a16(size_t(2) * OX_NM * WAVE * 4);
+        MLP = o;  o += a16(size_t(2) * OX_NW * WAVE * 4);           // M parts: [parity][wave][lane]
         REC = o;  o += a16(size_t(2) * OR_SETS * OX_RF * WAVE * 4 + 16);
         CL = o;   o += a16(size_t(C) + size_t(NP));
         FR = o;   o += a16(size_t(2) * OR_SETS * OX_FF * WAVE * 4);
@@ -67,6 +89,48 @@ struct OrLay {
         BYTES = o;
     }
 };
+
+// Multiloop-sum work of a diagonal with nls lane-sets: items qmb(ls) and
+// r2(ls), each cut into np parts (split-point ranges), one part per M wave
+// (8-15; their global loads wait on L2, so the sums get as many waves as the
+// interior loops).  Code: 0 = none, else 1 | isq << 1 | ls << 2 | pi << 4 | (np-1) << 6.
+__host__ __device__ constexpr int mcode(bool isq, int ls, int pi, int np) {
+    return 1 | (isq ? 2 : 0) | (ls << 2) | (pi << 4) | ((np - 1) << 6);
+}
+__device__ __forceinline__ int massign(int nls, int w) {
+    constexpr int Q = 1, R = 0;
+    if (nls >= 3) {
+        switch (w) {
+            case 8: return mcode(Q, 0, 0, 2);
+            case 9: return mcode(Q, 0, 1, 2);
+            case 10: return mcode(Q, 1, 0, 1);
+            case 11: return mcode(Q, 2, 0, 1);
+            case 12: return mcode(R, 0, 0, 1);
+            case 13: return mcode(R, 1, 0, 1);
+            case 14: return mcode(R, 2, 0, 2);
+            case 15: return mcode(R, 2, 1, 2);
+            default: return 0;
+        }
+    }
+    if (nls == 2) {
+        switch (w) {
+            case 8: return mcode(Q, 0, 0, 2);
+            case 9: return mcode(Q, 0, 1, 2);
+            case 10: return mcode(Q, 1, 0, 1);
+            case 11: return mcode(R, 0, 0, 2);
+            case 12: return mcode(R, 0, 1, 2);
+            case 13: return mcode(R, 1, 0, 3);
+            case 14: return mcode(R, 1, 1, 3);
+            case 15: return mcode(R, 1, 2, 3);
+            default: return 0;
+        }
+    }
+    if (nls == 1) {
+        if (w >= 8 && w < 12) return mcode(Q, 0, w - 8, 4);
+        if (w >= 12 && w < 16) return mcode(R, 0, w - 12, 4);
+    }
+    return 0;
+}
 
 // One workgroup per (walker, outside variant).  pair_p: [W][n_pairs].
 __global__ void __launch_bounds__(OX_NT, 1)
@@ -112,6 +176,10 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
     const int C = Y.C, NP = Y.NP;
     const DevTables &T = *ka.T;
+#ifdef ADX_STAMP
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- the proposal's inside tables (pf_ring_kernel's slot: qb, qm, qm1
     // diagonal-major, q5), at the variant's groups2 position
@@ -201,6 +269,7 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         G[k] = src[off(jc - ic, N) + ic - 1] * (ct[CT_INVMM + cc] * e);   // non-pairable: -0 * x = 0
     }
     __syncthreads();
+    OSTAMP(0);   // loads + the exterior-factor pass
 
     // ---- exterior adjoint (outside_cells.hip, three lane-sets of m)
     if (wid == 0) {
@@ -274,6 +343,7 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
     __syncthreads();
     for (int k = tid; k < C + OR_SLACK; k += OX_NT) L.yr[k] = 0.f;   // G's region: Y from here on
     __syncthreads();
+    OSTAMP(1);   // exterior adjoint, window, rank lists
 
     const float mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing, pw1 = XS->pwml[1];
     auto cell_of = [&](int D, int ls, int &i, int &j) {
@@ -392,17 +462,15 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         const int i = 1 + fl * WAVE + lane;
         if (i > N - e) return;
         const int j = i + e;
-        const float *mp = L.mlp + pe * OX_NM * WAVE + lane;
-        float qmbv, r2;
-        if (nle >= 3) {
-            qmbv = mp[fl * WAVE];
-            r2 = mp[(3 + fl) * WAVE];
-        } else if (nle == 2) {
-            qmbv = fl ? mp[2 * WAVE] : mp[0] + mp[WAVE];
-            r2 = fl ? mp[4 * WAVE] + mp[5 * WAVE] : mp[3 * WAVE];
-        } else {
-            qmbv = mp[0] + mp[WAVE] + mp[2 * WAVE];
-            r2 = mp[3 * WAVE] + mp[4 * WAVE] + mp[5 * WAVE];
+        const float *mp = L.mlp + pe * OX_NW * WAVE + lane;
+        float qmbv = 0.f, r2 = 0.f;   // the parts of this lane-set's items (massign)
+#pragma unroll
+        for (int w2 = 0; w2 < OX_NW; w2++) {
+            const int c = massign(nle, w2);
+            if (c && ((c >> 2) & 3) == fl) {
+                if (c & 2) qmbv += mp[w2 * WAVE];
+                else r2 += mp[w2 * WAVE];
+            }
         }
         const float R = i >= 2 ? pw1 * (L.rq[pn * NP + i - 1] + L.rr[pn * NP + i - 1]) : 0.f;
         const float chain = j < N ? mlbase_sig * L.r1[pn * NP + i] : 0.f;
@@ -412,7 +480,7 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         float a_int = 0.f;
         const float *pp = L.part + (pe * OR_SETS + fl) * OX_NB * WAVE + lane;
 #pragma unroll
-        for (int b = 0; b < OX_NB; b++) a_int += pp[b * WAVE];
+        for (int b = 0; b < OR_NB; b++) a_int += pp[b * WAVE];
         if (N - 3 - e < 0) a_int = 0.f;
         L.rq[pe * NP + i] = qmbv;
         L.rr[pe * NP + i] = R;
@@ -438,6 +506,119 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         L.qw[wo] = qbbm;
         L.ow[wo] = uint8_t((tp >> 8) & 255);
     };
+    // one part of a multiloop-sum item of diagonal d (massign): qmb or r2 of
+    // lane-set ls, split points pi / np of the lane-set's longest range
+    auto mpart = [&](int d, bool isq, int ls, int pi, int np) {
+        int i = 1 + ls * WAVE + lane;
+        const int ilast = min(N - d, (ls + 1) * WAVE);
+        if (i > N - d) i = N - d;
+        const int j = i + d;
+        float acc = 0.f, acc1 = 0.f;
+        constexpr int MB = 8;
+        // both sums read the slot in batches of MB terms, four batches in flight
+        // (a batch's global loads are issued three batches before it is summed)
+        if (isq) {
+            // qmb: t = 0 .. N-j-5: Y(i, j+5+t) = YR[rowb(i) + d + 1 + t] (LDS),
+            // qm1(j+1, j+5+t) on diagonal t+4 at position j (slot, coalesced)
+            const int lim = N - j - 5;
+            const int Tq = N - (1 + ls * WAVE + d) - 4;
+            const int ta = (Tq * pi) / np, tb = (Tq * (pi + 1)) / np;
+            const float *py = L.yr + rowb(i, N) + d + 1;
+            auto ld = [&](float (&q)[MB], int t) __attribute__((always_inline)) {
+#pragma unroll
+                for (int k = 0; k < MB; k++) q[k] = q1g[off(min(t + k, N - 5) + 4, N) + j];
+            };
+            auto use = [&](const float (&q)[MB], int t) __attribute__((always_inline)) {
+                float yv[MB];
+#pragma unroll
+                for (int k = 0; k < MB; k++) yv[k] = py[t + k];
+#pragma unroll
+                for (int k = 0; k < MB; k += 2) {
+                    acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, q[k], acc);
+                    acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, q[k + 1], acc1);
+                }
+            };
+            float qa[MB], qb[MB], qc[MB], qd[MB];
+            int t = ta;
+            if (t < tb) ld(qa, t);
+            if (t + MB < tb) ld(qb, t + MB);
+            if (t + 2 * MB < tb) ld(qc, t + 2 * MB);
+            while (t < tb) {
+                if (t + 3 * MB < tb) ld(qd, t + 3 * MB);
+                use(qa, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qa, t + 3 * MB);
+                use(qb, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qb, t + 3 * MB);
+                use(qc, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qc, t + 3 * MB);
+                use(qd, t);
+                t += MB;
+            }
+        } else {
+            // r2: u = 5 .. i-1 (ip = i - u): Y(i-u, j) = YR[rowb(i-u) + d + u - 4]
+            // (LDS), qm(i-u, i-1) on diagonal u-1 at position i-u-1 (slot, coalesced)
+            const int lim = i - 1;
+            const int Tr = ilast - 5;
+            const int ua = 5 + (Tr * pi) / np, ub = 5 + (Tr * (pi + 1)) / np;
+            auto ld = [&](float (&q)[MB], int u) __attribute__((always_inline)) {
+#pragma unroll
+                for (int k = 0; k < MB; k++) {
+                    const int uu = u + k;
+                    const bool ok = uu <= lim && uu < ub;
+                    q[k] = qmg[off(min(uu, N - 1) - 1, N) + (ok ? i - uu - 1 : 0)];
+                }
+            };
+            auto use = [&](const float (&q)[MB], int u) __attribute__((always_inline)) {
+                // Y(i-u-k, j): the row base moves by (i - u - k - N + 3) per term
+                const int ip0 = max(i - u, 1);
+                const int a0 = rowb(ip0, N) + d + u - 4;
+                const int D0 = i - u - N + 3;
+                float yv[MB];
+#pragma unroll
+                for (int k = 0; k < MB; k++) {
+                    const int uu = u + k;
+                    const bool ok = uu <= lim && uu < ub;
+                    const int a = a0 + k * D0 - (k * (k - 1)) / 2;
+                    yv[k] = L.yr[ok ? a : a0];
+                    yv[k] = ok ? yv[k] : 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < MB; k += 2) {
+                    acc = fmaf(yv[k], q[k], acc);
+                    acc1 = fmaf(yv[k + 1], q[k + 1], acc1);
+                }
+            };
+            float qa[MB], qb[MB], qc[MB], qd[MB];
+            int u = ua;
+            if (u < ub) ld(qa, u);
+            if (u + MB < ub) ld(qb, u + MB);
+            if (u + 2 * MB < ub) ld(qc, u + 2 * MB);
+            while (u < ub) {
+                if (u + 3 * MB < ub) ld(qd, u + 3 * MB);
+                use(qa, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qa, u + 3 * MB);
+                use(qb, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qb, u + 3 * MB);
+                use(qc, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qc, u + 3 * MB);
+                use(qd, u);
+                u += MB;
+            }
+        }
+        return acc + acc1;
+    };
     auto fin = [&](int d) {
         if (wid < OR_SETS) {
             finalize(d, wid);
@@ -450,100 +631,36 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         }
     };
 
-    if (wid < OX_NB) {
+    if (wid < OR_NB) {
         switch (wid) {
-            case 0: b_sweep<OR_SETS, 19, -1, -1, -1, -1>(L, N, lane, wid, fin); break;
-            case 1: b_sweep<OR_SETS, 5, 7, 15, -1, -1>(L, N, lane, wid, fin); break;
-            case 2: b_sweep<OR_SETS, 4, 0, 23, -1, -1>(L, N, lane, wid, fin); break;
-            case 3: b_sweep<OR_SETS, 3, 30, 6, 11, -1>(L, N, lane, wid, fin); break;
-            case 4: b_sweep<OR_SETS, 29, 28, 27, 1, -1>(L, N, lane, wid, fin); break;
-            case 5: b_sweep<OR_SETS, 26, 25, 24, 2, -1>(L, N, lane, wid, fin); break;
-            case 6: b_sweep<OR_SETS, 22, 21, 20, 8, -1>(L, N, lane, wid, fin); break;
-            case 7: b_sweep<OR_SETS, -1, -1, -1, -1, -1>(L, N, lane, wid, fin); break;
-            case 8: b_sweep<OR_SETS, 18, 17, 16, 10, -1>(L, N, lane, wid, fin); break;
-            default: b_sweep<OR_SETS, 14, 13, 12, 9, -1>(L, N, lane, wid, fin); break;
+            // loop sizes in blocks of about equal cost (a size >= 6: 3 reads for its
+            // special shapes + one per 4 generic ones per lane-set; sizes <= 5 ~3 per
+            // shape), a little less on the finalize (0-2) and record (7) waves
+            case 0: b_sweep<OR_SETS, 28, 20, 13, 0, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 1: b_sweep<OR_SETS, 27, 21, 1, 7, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 2: b_sweep<OR_SETS, 26, 22, 12, 6, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 3: b_sweep<OR_SETS, 4, 19, 14, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 4: b_sweep<OR_SETS, 3, 24, 16, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 5: b_sweep<OR_SETS, 30, 25, 18, 11, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 6: b_sweep<OR_SETS, 5, 23, 15, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            default: b_sweep<OR_SETS, 29, 2, 17, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
         }
     } else for (int d = N - 1; d >= 3; d--) {
         const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;
         const int par = d & 1;
-        const int mw = wid - OX_NB;
         if (d >= 4) {
-            // ---------------- M: multiloop adjoint sums of diagonal d.  Items: qmb and
-            // r2 per lane-set; three lane-sets: one item per wave; two: qmb ls0 in
-            // halves, qmb ls1, r2 ls0, r2 ls1 in halves; one: qmb and r2 in thirds
-            bool isq;
-            int ls, np, pi;
-            if (nls >= 3) {
-                isq = mw < 3;
-                ls = isq ? mw : mw - 3;
-                np = 1;
-                pi = 0;
-            } else if (nls == 2) {
-                isq = mw < 3;
-                ls = (mw == 2 || mw >= 4) ? 1 : 0;
-                np = (mw <= 1 || mw >= 4) ? 2 : 1;
-                pi = (mw == 1 || mw == 5) ? 1 : 0;
-            } else {
-                isq = mw < 3;
-                ls = 0;
-                np = 3;
-                pi = mw % 3;
-            }
-            int i = 1 + ls * WAVE + lane;
-            const int ilast = min(N - d, (ls + 1) * WAVE);
-            if (i > N - d) i = N - d;
-            const int j = i + d;
-            float acc = 0.f, acc1 = 0.f;
-            if (isq) {
-                // qmb: t = 0 .. N-j-5: Y(i, j+5+t) = YR[rowb(i) + d + 1 + t] (LDS),
-                // qm1(j+1, j+5+t) on diagonal t+4 at position j (slot, coalesced)
-                const int lim = N - j - 5;
-                const int Tq = N - (1 + ls * WAVE + d) - 4;
-                const int ta = (Tq * pi) / np, tb = (Tq * (pi + 1)) / np;
-                const float *py = L.yr + rowb(i, N) + d + 1;
-                for (int t = ta; t < tb; t += 16) {
-                    float yv[16], qv[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int tt = min(t + k, N - 5);
-                        qv[k] = q1g[off(tt + 4, N) + j];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 16; k++) yv[k] = py[t + k];
-#pragma unroll
-                    for (int k = 0; k < 16; k += 2) {
-                        acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, qv[k], acc);
-                        acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, qv[k + 1], acc1);
-                    }
-                }
-            } else {
-                // r2: u = 5 .. i-1 (ip = i - u): Y(i-u, j) = YR[rowb(i-u) + d + u - 4]
-                // (LDS, the base moves by (i - u - N + 3) per term), qm(i-u, i-1) on
-                // diagonal u-1 at position i-u-1 (slot, coalesced)
-                const int lim = i - 1;
-                const int Tr = ilast - 5;
-                const int ua = 5 + (Tr * pi) / np, ub = 5 + (Tr * (pi + 1)) / np;
-                for (int u = ua; u < ub; u += 16) {
-                    float yv[16], qv[16];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int uu = u + k;
-                        const bool ok = uu <= lim && uu < ub;
-                        const int ip = ok ? i - uu : 1;
-                        qv[k] = qmg[off(min(uu, N - 1) - 1, N) + (ok ? ip - 1 : 0)];
-                        yv[k] = ok ? L.yr[rowb(ip, N) + d + uu - 4] : 0.f;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 16; k += 2) {
-                        acc = fmaf(yv[k], qv[k], acc);
-                        acc1 = fmaf(yv[k + 1], qv[k + 1], acc1);
-                    }
-                }
-            }
-            L.mlp[(par * OX_NM + mw) * WAVE + lane] = acc + acc1;
+            // ---------------- M: the multiloop-sum parts of diagonal d on this wave
+            const int c = massign(nls, wid);
+            if (c) L.mlp[(par * OX_NW + wid) * WAVE + lane] = mpart(d, (c & 2) != 0, (c >> 2) & 3, (c >> 4) & 3, (c >> 6) + 1);
         }
+        OSTAMP(4);   // M sums
         lds_barrier();
+        OSTAMP(6);   // barrier
     }
+#ifdef ADX_STAMP
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_stamps_or[wid][k], st_acc[k]);
+#endif
     // ---- requested pairs of this fold, the motif's inner pairs credited from
     // its closing cell (outside_cells.hip)
     double *pp = pair_p + size_t(w) * ka.n_pairs;

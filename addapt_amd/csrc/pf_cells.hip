@@ -590,6 +590,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
     }
     __syncthreads();
+    PSTAMP(7);   // motif sites + the restore's stores (the wait for its loads)
     const uint8_t *S = L.S;
     const float *ct = L.ct;
     const float sig1 = XS->sig[1], mlbase_sig = XS->mlbase_sig, mlclosing = XS->mlclosing;

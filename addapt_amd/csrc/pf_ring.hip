@@ -12,7 +12,9 @@
 //     finalised cell to the walker's table slot (diagonal-major, as pf_cells),
 //     the prep stage stores the restored and non-pairable cells, and Q reads
 //     column j from there two steps after it is final (a global read per lane
-//     and lane-set, issued a step ahead);
+//     and lane-set, issued a step ahead; every writer drains its stores at the
+//     start of its next step, so no wave waits on a store on its way to the
+//     barrier);
 //   * the slot keeps qm and qm1 DIAGONAL-major (not row- / column-major as
 //     pf_cells): the outside pass for these lengths (outside_ring.hip) reads
 //     them from the slot with lanes = cells, where a diagonal-major table makes
@@ -21,11 +23,12 @@
 // One step = one anti-diagonal, ONE barrier:
 //   B  (waves 0-6)  interior-loop sums of diagonal s (pf_cells' blocks)
 //   F  (wave 7)     cells of diagonal s-1: qb, qm1, the slot store
-//   Q  (wave 8)     q5[s-2] from column s-2 (loaded last step), the load of
-//                   column s-1, and the PREP of diagonal s+1: inner codes,
-//                   hairpin (+ motif) initial values of the changed cells,
-//                   restored values of the others (loaded a step ahead)
+//   Q  (wave 8)     q5[s-3] from column s-3 (loaded last step), the load of
+//                   column s-2
 //   R  (wave 9)     setup records of the B lanes, four stages a step apart
+//   prep            of diagonal s+1, one lane-set each on M waves 12, 13 and R: inner
+//                   codes, hairpin (+ motif) initial values of the changed
+//                   cells, restored values of the others (loaded a step ahead)
 //   M  (waves 10-13) qm items of span s-2
 #include <hip/hip_runtime.h>
 
@@ -265,11 +268,29 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_add(float v) {
     return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float wave_sum_r(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+// sum over the wave, uniform result: DPP row sums, then the four rows' totals
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = dpp_add<0xb1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x114>(v);   // row_shr:4
+    v = dpp_add<0x118>(v);   // row_shr:8 -> lane 15 of each row holds the row sum
+    const int b = __float_as_int(v);
+    return __int_as_float(__builtin_amdgcn_readlane(b, 15)) + __int_as_float(__builtin_amdgcn_readlane(b, 31)) +
+           __int_as_float(__builtin_amdgcn_readlane(b, 47)) + __int_as_float(__builtin_amdgcn_readlane(b, 63));
 }
+#ifdef ADX_STAMP
+// Diagnostic build only: per-wave cycle sums of the phases (s_memtime), read
+// back through adx_debug_stamps_ring().  Never in the product.
+__device__ unsigned long long g_stamps_r[16][8];
+#define RSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#define RG_STP_PARAMS , unsigned long long *st_acc, unsigned long long &st_last
+#define RG_STP_ARGS , st_acc, st_last
+#else
+#define RSTAMP(k) do { } while (0)
+#define RG_STP_PARAMS
+#define RG_STP_ARGS
+#endif
+
 // global stores of this wave complete before the step's barrier (the slot is
 // read back by Q within the workgroup)
 __device__ __forceinline__ void vm_drain() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -277,7 +298,7 @@ __device__ __forceinline__ void vm_drain() { __asm__ volatile("s_waitcnt vmcnt(0
 // B: interior-loop sums of every diagonal for one block of loop sizes (pf_cells.hip pb_sweep)
 template <int U0, int U1, int U2, int U3, int U4>
 __device__ __forceinline__ void rb_sweep(const RgL &L, const DevScaled *XS, int N, int lane, int wid,
-                                         bool constrained, int s_end) {
+                                         bool constrained, int s_end RG_STP_PARAMS) {
     constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
     constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
     constexpr bool H5 = U0 == 5 || U1 == 5 || U2 == 5 || U3 == 5 || U4 == 5;
@@ -322,6 +343,7 @@ __device__ __forceinline__ void rb_sweep(const RgL &L, const DevScaled *XS, int 
             }
             const float outer = r < 2 ? c.tau : c.mo;
             float g = 0.f, sp = 0.f, gs = 0.f, sps = 0.f;
+            RSTAMP(1);   // B cell records
             const bool mk = constrained && __ballot((fl >> 27) & 1) != 0;
             if (mk) {
                 rg_run<U0, true>(s0, L, c, s, umax, r, ctb, outer, g, sp, gs, sps);
@@ -339,8 +361,11 @@ __device__ __forceinline__ void rb_sweep(const RgL &L, const DevScaled *XS, int 
             const float part = quad_sum_r(fmaf(g, mmo, sp) + (r == 0 ? fmaf(gs, mmo, sps) : 0.f));
             if (r == 0 && idx < ncell && ((fl >> 28) & 1))
                 L.part[((par * RG_SETS + ((c.i - 1) >> 6)) * RG_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] = part;
+            RSTAMP(2);   // B shapes
         }
+        RSTAMP(3);
         lds_barrier();
+        RSTAMP(7);   // barrier
     }
 }
 
@@ -395,6 +420,10 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
     const int C = Y.C, NP = Y.NP, RS = Y.RS;
     const DevTables &T = *ka.T;
+#ifdef ADX_STAMP
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- incremental fold state (pf_cells.hip): this variant's tables of the
     // current sequence (src) and the proposal's (dst), diagonal-major
@@ -561,28 +590,24 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     }
     __syncthreads();
 
-    // ---- prep of diagonal D into the ring (wave Q): inner codes; the changed
-    // cells' hairpin (+ motif) initial values or the non-pairable mark (-0,
-    // also stored to the slot); the restored values of the others (loaded one
-    // step ahead: rload) and their slot copies
-    float rsv[RG_SETS] = {0.f, 0.f, 0.f};
-    auto rload = [&](int D) {
+    // ---- prep of lane-set h of diagonal D into the ring (lane-sets 0, 1, 2 on
+    // waves 12, 13 and R): inner codes; the changed cells' hairpin (+ motif)
+    // initial values or the non-pairable mark (-0, also stored to the slot); the
+    // restored values of the others (loaded one step ahead: rload) and their
+    // slot copies
+    float rsv = 0.f;
+    auto rload = [&](int D, int h) {
         if (!incr || D < 4 || D > N - 1) return;
         const int od = off(D, N), lo = clo(D), hi = chi(D);
-#pragma unroll
-        for (int h = 0; h < RG_SETS; h++) {
-            const int i = 1 + h * WAVE + lane;
-            if (h * WAVE < N - D && i <= N - D && (i < lo || i > hi)) rsv[h] = src[od + i - 1];
-        }
+        const int i = 1 + h * WAVE + lane;
+        if (h * WAVE < N - D && i <= N - D && (i < lo || i > hi)) rsv = src[od + i - 1];
     };
-    auto prep = [&](int D) {
+    auto prep = [&](int D, int h) {
         if (D < 4 || D > N - 1) return;
         const int od = off(D, N), ro = rgo(D, RS), lo = clo(D), hi = chi(D);
-#pragma unroll
-        for (int h = 0; h < RG_SETS; h++) {
+        {
             const int i = 1 + h * WAVE + lane;
-            if (h * WAVE >= N - D) break;
-            if (i > N - D) continue;
+            if (h * WAVE >= N - D || i > N - D) return;
             const int j = i + D;
             const int type = ptype(S[i], S[j]);
             L.cc[ro + i - 1] = uint8_t(rtype(type) * 25 + S[j + 1] * 5 + S[i - 1]);
@@ -613,11 +638,13 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                 }
                 L.qb[ro + i - 1] = init;
             } else {   // restored (final)
-                L.qb[ro + i - 1] = rsv[h];
-                qbg[od + i - 1] = rsv[h];
+                L.qb[ro + i - 1] = rsv;
+                qbg[od + i - 1] = rsv;
             }
         }
     };
+    // this wave's prep lane-set: the two M waves with the fewest items and R
+    const int ph = wid == 12 ? 0 : wid == 13 ? 1 : wid == RG_WR ? 2 : -1;
 
     // ---- records (wave R): pf_cells.hip's four stages, three lane-sets
     struct Pend {
@@ -721,11 +748,11 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
         seqp = seq_load(6, idx_load(6));
         idxp = idx_load(7);
     }
-    if (wid == RG_WQ) {   // diagonal 4 before the sweep, diagonal 5's restored values in flight
-        rload(4);
-        prep(4);
+    if (ph >= 0) {   // diagonal 4 before the sweep, diagonal 5's restored values in flight
+        rload(4, ph);
+        prep(4, ph);
         vm_drain();
-        rload(5);
+        rload(5, ph);
     }
     __syncthreads();
 
@@ -751,16 +778,17 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
             qv[h] = ok && h * WAVE < j - 4 ? qbg[off(j - k, N) + k - 1] : 0.f;
         }
     };
-    const int s_end = N + 2;   // Q finishes q5[N] two steps after column N is final
+    const int s_end = N + 3;   // Q finishes q5[N] three steps after column N is final
+    RSTAMP(0);   // setup
     if (wid < RG_NB) {
         switch (wid) {
-            case 0: rb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end); break;
-            case 1: rb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end); break;
-            case 2: rb_sweep<3, 20, 18, 8, 6>(L, XS, N, lane, wid, constrained, s_end); break;
-            case 3: rb_sweep<28, 26, 1, 9, 7>(L, XS, N, lane, wid, constrained, s_end); break;
-            case 4: rb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end); break;
-            case 5: rb_sweep<30, 2, 17, 14, -1>(L, XS, N, lane, wid, constrained, s_end); break;
-            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end); break;
+            case 0: rb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 1: rb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 2: rb_sweep<3, 20, 18, 8, 6>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 3: rb_sweep<28, 26, 1, 9, 7>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 4: rb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 5: rb_sweep<30, 2, 17, 14, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
         }
     } else {
         __builtin_amdgcn_s_setprio(2);
@@ -772,12 +800,14 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                     const int lo = qlo(sq), n = qhi(sq) - lo + 1;
                     int K = 16;
                     while (K > 1 && (N - sq) * K > RG_NMW * WAVE) K >>= 1;
-                    const int ipw = WAVE / K;
                     const int mw = rg_mw(wid);
                     const int k = lane & (K - 1);
-                    const int item0 = mw * ipw;
-                    for (int it0 = item0; it0 < n; it0 += RG_NMW * ipw) {   // more items than lanes: rounds
-                        const int item = it0 + lane / K;
+                    // K and the split ranges follow the full fold's item count, so a
+                    // refold sums every item as a fold from scratch does (n <= N - sq
+                    // <= RG_NMW * WAVE / K: one round)
+                    const int ipw = WAVE / K;
+                    if (mw * ipw < n) {
+                        const int item = mw * ipw + lane / K;
                         const bool valid = item < n;
                         const int i = lo + (valid ? item : n - 1);
                         const int jb = i + sq, T = sq - 4;
@@ -816,7 +846,18 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                         }
                     }
                 }
+                if (ph >= 0) {
+                    // the prep of lane-set ph of diagonal s + 1 (its restored values were
+                    // loaded last step); the drain first completes last step's prep
+                    // stores (read by Q two steps on) and loads, a step old by now
+                    RSTAMP(5);
+                    vm_drain();
+                    prep(s + 1, ph);
+                    RSTAMP(6);
+                    rload(s + 2, ph);   // in flight across the barrier
+                }
             } else if (wid == RG_WF) {
+                vm_drain();        // last step's finalised cells (Q loads them this step)
                 // ---------------- F: the changed cells of diagonal e = s - 1
                 const int e = s - 1;
                 if (e >= 4 && e <= N - 1) {
@@ -853,10 +894,9 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                         }
                     }
                 }
-                vm_drain();
             } else if (wid == RG_WQ) {
-                // ---------------- Q: q5[j], j = s - 2, from column j loaded last step
-                const int j = s - 2;
+                // ---------------- Q: q5[j], j = s - 3, from column j loaded last step
+                const int j = s - 3;
                 if (j >= 4 && j <= N && (!incr || j >= m_lo - 1)) {
                     float acc = 0.f;
                     if (qcol == j) {
@@ -868,24 +908,33 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                             acc = fmaf(L.q5[k - 1] * qv[h], qf[h], acc);
                         }
                     }
-                    acc = wave_sum_r(acc);
+                    acc = wave_sum_dpp(acc);
                     if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sig1 : 0.f) + acc;
                 }
-                prep(s + 1);       // diagonal s + 1 into the ring (its restored values loaded last step)
-                vm_drain();        // the prep's slot stores (nothing else is outstanding here)
-                // loads issued after the drain stay in flight across the barrier
-                rload(s + 2);
-                qload(s - 1);      // column s - 1 is final (its last cell, (1, s-1), was finalised last step)
+                RSTAMP(5);         // q5
+                // column s - 2 is final: its last cell, (1, s-2), was finalised two steps
+                // ago and its store drained by F at the start of the last step
+                qload(s - 2);
             } else if (wid == RG_WR) {
+                vm_drain();        // last step's prep stores and loads (the record loads are a step old)
+                prep(s + 1, 2);
+                rload(s + 2, 2);
                 rec_store(s + 1, pend);
                 pend = rec_load(s + 2, seqp);
                 seqp = seq_load(s + 3, idxp);
                 idxp = idx_load(s + 4);
             }
+            RSTAMP(3);   // the role's step work
             lds_barrier();
+            RSTAMP(7);   // barrier
         }
     }
     __syncthreads();
+    RSTAMP(4);
+#ifdef ADX_STAMP
+    if (lane == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_stamps_r[wid][k], st_acc[k]);
+#endif
     // ---- the proposal's qm / qm1 to the slot, diagonal-major (qb is there already)
     if (dst) {
         for (int D = 4 + wid; D <= N - 1; D += RG_NW) {
@@ -934,3 +983,14 @@ hipError_t launch_pf_ring(const KArgs &ka, const uint8_t *seqs, int W, const int
 }
 
 }  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps_ring(unsigned long long *out, int reset) {  // [16][8]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_r), sizeof(adx::g_stamps_r)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_r), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Per-wave phase breakdown of outside_cells_kernel (diagnostic stamp build:
-ADX_LIB=addapt_amd/_lib/ablate/lib_stamp.so).  Runs config-3 MC steps.
+"""Per-wave phase breakdown of the lanes = cells outside kernels (diagnostic
+stamp build: ADX_LIB=addapt_amd/_lib/ablate/lib_stamp.so).  Runs config-3
+MC steps (N = 100: outside_cells_kernel) or config-4 ones (N > 100:
+outside_ring_kernel, its own stamp table).
 usage: outside_stamps.py [N] [W] [steps]"""
 import ctypes as C
 import os
@@ -10,8 +12,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from addapt_amd import native, workloads  # noqa: E402
 
 L = native.lib()
-L.adx_debug_stamps_outside.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+read = L.adx_debug_stamps_outside_ring if N > 100 else L.adx_debug_stamps_outside
+read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 tmpl, active = workloads.synthetic(N)
@@ -22,9 +25,9 @@ seqs = workloads.walker_sequences(tmpl, [active], W)
 eng.walkers_init(list(range(W)), seqs)
 eng.run_steps(1)
 buf = (C.c_ulonglong * 128)()
-L.adx_debug_stamps_outside(buf, 1)
+read(buf, 1)
 eng.run_steps(steps)
-L.adx_debug_stamps_outside(buf, 1)
+read(buf, 1)
 _, _, c = eng.download()
 scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = 2 * scored   # outside folds (apo, holo) of the scored walkers

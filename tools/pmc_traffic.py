@@ -17,7 +17,8 @@ import sys
 
 # the kernels of one step's score window (kernels.hip, mfe_cells.hip, pf_cells.hip, outside_cells.hip):
 # the fold kernels, and with pair terms the outside pass and the score combine
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "pf_cells_kernel", "outside_cells_kernel", "bppm_kernel", "combine_kernel")
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "pf_cells_kernel", "pf_ring_kernel", "outside_cells_kernel",
+                 "outside_ring_kernel", "bppm_kernel", "combine_kernel")
 
 
 def per_kernel(path, counter):
@@ -45,7 +46,10 @@ def main():
         total += b
         kernels[name] = {"fetch_size_kb_raw": fk, "write_size_kb": wk, "bytes": b,
                          "launches": f.get(name, (0, 0))[1]}
-    out = {"kernel": "score_kernel", "kernels": kernels, "bytes_per_launch": total,
+    # the kernel with the most bytes per launch (short name, as rocprof lists it)
+    top = max(kernels, key=lambda k: kernels[k]["bytes"]) if kernels else ""
+    short = top.replace("(anonymous namespace)::", "").replace("void ", "").replace("adx::", "").split("(")[0]
+    out = {"kernel": short, "kernels": kernels, "bytes_per_launch": total,
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM); KB = 1024 B"}
     print(json.dumps(out, indent=1))
 
