@@ -15,10 +15,38 @@ spec.loader.exec_module(G)
 
 
 def test_partitions_cover_each_loop_size_once():
-    blocks, load = G.partition()
-    sizes = sorted(u for b in blocks for u in b)
-    assert sizes == list(range(G.MAXLOOP + 1))
-    assert len(blocks) == G.NBLK and max(load) - min(load) <= 10
+    for S in (1, 2, 4):   # one partition per lanes-per-cell mode
+        blocks, load = G.partition(S)
+        sizes = sorted(u for b in blocks for u in b)
+        assert sizes == list(range(G.MAXLOOP + 1))
+        assert len(blocks) == G.NBLK and max(load) - min(load) <= 10, (S, load)
+
+
+def _slice_edges(S, r, u):
+    """mfe_cells.hip B setup: slice r's (ea, eb) and the edge n1 it reads."""
+    eb = r & 1
+    ea = ((-(r >> 1)) if (r & 1) else (r >> 1)) if S == 4 else (-1 if (r & 1) else 1)
+    return [ea + eb * u] if S == 4 else [eb * u, ea + eb * u]
+
+
+def test_sliced_edge_shapes_once_per_cell():
+    """Sizes u >= 4 read their bulges and 1 x n loops on one slice each (4 lanes
+    per cell) or two per slice (2 lanes per cell); the kinds match the table the
+    slice uses (CT_BUL on slices 0, 1, CT_ONEN on 2, 3)."""
+    for u in range(4, G.MAXLOOP + 1):
+        for S in (2, 4):
+            got = sorted(n for r in range(S) for n in _slice_edges(S, r, u))
+            assert got == sorted(G.edges(u)), (S, u, got)
+        for r in range(4):
+            (n1,) = _slice_edges(4, r, u)
+            assert G.kind(n1, u - n1) == ("1n" if r & 2 else "bul"), (u, r)
+        for r in range(2):
+            b, n = _slice_edges(2, r, u)
+            assert G.kind(b, u - b) == "bul" and G.kind(n, u - n) == "1n"
+        pre, decl, lines, outs, ins, post = G.sliced_parts(u, 4, "a")
+        # the edge shapes are not also read at fixed offsets
+        fixed = {int(ln.split("offset:")[1]) // 4 for ln in lines if "%[qaa] offset:" in ln}
+        assert not fixed & set(G.edges(u)), (u, fixed)
 
 
 def test_shape_kinds():

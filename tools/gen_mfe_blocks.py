@@ -62,15 +62,33 @@ def ucost(u):
     return sum(COST[kind(u1, u - u1)] for u1 in range(u + 1))
 
 
-def partition():
+def edges(u):
+    """The four edge shapes of a loop size u >= 4 -- bulges (0,u) (u,0), 1 x n
+    loops (1,u-1) (u-1,1) -- spread over the lane slices of a sliced block."""
+    return [0, u, 1, u - 1] if u >= 4 else []
+
+
+def scost(u, S):
+    """LDS cost per lane of loop size u in a block with S lanes per cell: the
+    edge shapes spread over the slices, other special shapes in every slice,
+    generic shapes 1/S each."""
+    if S == 1:
+        return ucost(u)
+    e = edges(u)
+    spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen" and u1 not in e]
+    ngen = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen")
+    return (len(e) // S) * 3 + sum(COST[kind(u1, u - u1)] for u1 in spec) + (ngen + S - 1) // S
+
+
+def partition(S=1):
     # greedy LPT over loop sizes, largest first; ties keep small u spread out
-    sizes = sorted(range(MAXLOOP + 1), key=lambda u: -ucost(u))
+    sizes = sorted(range(MAXLOOP + 1), key=lambda u: (-scost(u, S), -ucost(u)))
     blocks = [[] for _ in range(NBLK)]
     load = [0] * NBLK
     for u in sizes:
         b = min(range(NBLK), key=lambda k: (load[k], len(blocks[k])))
         blocks[b].append(u)
-        load[b] += ucost(u)
+        load[b] += scost(u, S)
     return [sorted(b) for b in blocks], load
 
 
@@ -205,8 +223,13 @@ def emit_table_fin(blk, out):
 def sliced_parts(u, S, t):
     """One loop size of a sliced block, variable names suffixed by t: address
     lines, declarations, asm reads/outputs/inputs and the arithmetic after the
-    batch."""
-    spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen"]
+    batch.  Loop sizes u >= 4 spread their edge shapes over the slices: with
+    S = 4 slice r reads edge n1 = C.ea + C.eb * u (bulges on slices 0, 1, 1 x n
+    on 2, 3: accumulator a.e, the outer term per slice is added by the caller),
+    with S = 2 slice r reads the bulge n1 = C.eb * u and the 1 x n loop
+    n1 = C.ea + C.eb * u."""
+    ed = edges(u)
+    spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen" and u1 not in ed]
     gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
     pre, decl, lines, outs, ins, post = [], [], [], [], [], []
     pre.append("const int o%s = off(dd - %d, U.N) + ci;" % (t, u + 2))
@@ -214,8 +237,25 @@ def sliced_parts(u, S, t):
     ins += ['[qa%s] "v"(qa%s)' % (t, t), '[ka%s] "v"(ka%s)' % (t, t)]
     V = lambda u1: "v%d%s" % (u1, t)
     Cc = lambda u1: "c%d%s" % (u1, t)
-    decl.append("uint32_t %s;" % ", ".join(V(u1) for u1 in spec))
-    decl.append("uint32_t %s;" % ", ".join(Cc(u1) for u1 in spec))
+    # edge reads: (name, per-lane n1 expression, kind)
+    eds = []
+    if ed and S == 4:
+        eds = [("e", "ea + eb * %d" % u, "edge")]
+    elif ed and S == 2:
+        eds = [("b", "eb * %d" % u, "bul"), ("n", "ea + eb * %d" % u, "1n")]
+    for nm, ex, _ in eds:
+        pre.append("const int n%s%s = %s;" % (nm, t, ex))
+        pre.append("const uint32_t q%s%s = qa%s + uint32_t(n%s%s) * 4u, k%s%s = ka%s + uint32_t(n%s%s);"
+                   % (nm, t, t, nm, t, nm, t, t, nm, t))
+        ins += ['[q%s%s] "v"(q%s%s)' % (nm, t, nm, t), '[k%s%s] "v"(k%s%s)' % (nm, t, nm, t)]
+        decl.append("uint32_t v%s%s, c%s%s;" % (nm, t, nm, t))
+        lines.append("ds_read_b32 %%[v%s%s], %%[q%s%s]" % (nm, t, nm, t))
+        outs.append('[v%s%s] "=&v"(v%s%s)' % (nm, t, nm, t))
+        lines.append("ds_read_u8 %%[c%s%s], %%[k%s%s]" % (nm, t, nm, t))
+        outs.append('[c%s%s] "=&v"(c%s%s)' % (nm, t, nm, t))
+    if spec:
+        decl.append("uint32_t %s;" % ", ".join(V(u1) for u1 in spec))
+        decl.append("uint32_t %s;" % ", ".join(Cc(u1) for u1 in spec))
     for u1 in spec:
         lines.append("ds_read_b32 %%[%s], %%[qa%s] offset:%d" % (V(u1), t, 4 * u1))
         outs.append('[%s] "=&v"(%s)' % (V(u1), V(u1)))
@@ -246,6 +286,8 @@ def sliced_parts(u, S, t):
     post.append("    const int ml = %d - C.B, mh = C.A, rr = int(C.rs >> 2);" % u)
     for u1 in spec:
         post.append("    %s = (%d >= ml && %d <= mh) ? %s : INF16;" % (V(u1), u1, u1, V(u1)))
+    for nm, _, _ in eds:
+        post.append("    v%s%s = (n%s%s >= ml && n%s%s <= mh) ? v%s%s : INF16;" % ((nm, t) * 4))
     for k in range(nk):
         post.append("    w%d%s = (%d + rr >= ml && %d + rr <= mh) ? w%d%s : INF16;" % (k, t, gen[0] + S * k, gen[0] + S * k, k, t))
     post.append("}")
@@ -254,6 +296,14 @@ def sliced_parts(u, S, t):
     if u >= 2:
         post.append("const uint32_t fb%s = kr1%s.z, f1n%s = kr1%s.w;" % (t, t, t, t))
         post.append("(void)fb%s; (void)f1n%s;" % (t, t))
+    for nm, _, k in eds:
+        v, c = "v%s%s" % (nm, t), "c%s%s" % (nm, t)
+        if k == "edge":
+            post.append("a.e = pmin(a.e, padd(%s, padd(U.ct[C.ctb + %s], C.r2 ? f1n%s : fb%s)));" % (v, c, t, t))
+        elif k == "bul":
+            post.append("a.b = pmin(a.b, padd(%s, padd(U.ct[CT_BUL + %s], fb%s)));" % (v, c, t))
+        else:
+            post.append("a.n = pmin(a.n, padd(%s, padd(U.ct[CT_ONEN + %s], f1n%s)));" % (v, c, t))
     for u1 in spec:
         k = kind(u1, u - u1)
         v, c = V(u1), Cc(u1)
@@ -363,10 +413,12 @@ def main():
     out.append("}")
     out.append("")
     for S in (2, 4):
-        for b, blk in enumerate(blocks):
+        sblocks, sload = partition(S)
+        out.append("// %d lanes per cell: blocks of LDS cost %s: %s" % (S, sload, "; ".join("%d:%s" % (b, blk) for b, blk in enumerate(sblocks))))
+        for b, blk in enumerate(sblocks):
             out.append("__device__ __forceinline__ void mfe_blk%d_s%d(const BUni &U, const BCell &C, Acc &a) {" % (b, S))
-            out.append("    int ci = C.i, dd = U.d, um = U.umax;")
-            out.append('    asm volatile("" : "+v"(ci));')
+            out.append("    int ci = C.i, dd = U.d, um = U.umax, ea = C.ea, eb = C.eb;")
+            out.append('    asm volatile("" : "+v"(ci), "+v"(ea), "+v"(eb));')
             out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
             emit_table_decl(blk, out)
             emit_block_cells_sliced(blk, S, out)
@@ -380,12 +432,14 @@ def main():
         out.append("    }")
         out.append("}")
         out.append("")
-    # which blocks hold the table shapes (prefetch only there)
-    tb = 0
-    for b, blk in enumerate(blocks):
-        if any(u in (2, 3, 4) for u in blk):
-            tb |= 1 << b
-    out.append("constexpr unsigned MFE_TABLE_BLOCKS = 0x%xu;   // blocks with 1x1 / 1x2 / 2x1 / 2x2 shapes" % tb)
+    # which blocks hold the table shapes (prefetch only there), per lanes per cell
+    for S in (1, 2, 4):
+        tb = 0
+        for b, blk in enumerate(partition(S)[0]):
+            if any(u in (2, 3, 4) for u in blk):
+                tb |= 1 << b
+        out.append("constexpr unsigned MFE_TABLE_BLOCKS%s = 0x%xu;   // blocks with 1x1 / 1x2 / 2x1 / 2x2 shapes%s"
+                   % ("" if S == 1 else "_S%d" % S, tb, "" if S == 1 else " (%d lanes per cell)" % S))
     out.append("constexpr int MFE_NBLK = %d;" % NBLK)
     out.append("constexpr int MFE_KSAT = %d;   // generic loops: nin[k] == nin[MFE_KSAT] for k >= MFE_KSAT" % KSAT)
     path = os.path.join(out_dir(), "mfe_blocks.inc")
