@@ -554,6 +554,16 @@ struct Problem {
              pack16(X16->pwml, NMAX + 1) && pack16(&X16->mlclosing, 1) && pack16(&X16->mlbase_sig, 1) &&
              pack16(X16->sp_val, MAX_SPECIAL_HP) && pack16(&X16->motif_extra, 1);
         if (!ok) return ADX_OK;   // FP32 MinPlus only
+        {   // mfe_cells.hip interior-loop records (both halves non-negative: a plain 32-bit add)
+            uint32_t il[32], nin[32], ct[CT_SIZE];
+            std::memcpy(il, X16->il, sizeof il);
+            std::memcpy(nin, X16->nin, sizeof nin);
+            std::memcpy(ct, X16->ctab, sizeof ct);
+            for (int u = 0; u < 32; u++)
+                for (int f = 0; f < 8; f++)
+                    X16->ku16[u][f] = f < 6 ? ((u >= 6 && u <= 30) ? il[u] + nin[f] : 0u)
+                                    : f == 6 ? ct[CT_FB + u] : (u >= 1 ? ct[CT_F1N + u - 1] : 0x7FFF7FFFu);
+        }
         HIP_TRY(dT16.upload(T16.get(), 1, stream));
         HIP_TRY(dX16.upload(X16.get(), 1, stream));
         HIP_TRY(hipStreamSynchronize(stream));

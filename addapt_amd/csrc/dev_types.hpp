@@ -79,6 +79,9 @@ struct DevScaled {
     // MFE only (mfe_cells.hip): generic interior energy = il[u] + nin[|n1 - n2|]
     float il[32];            // interior[u]
     float nin[32];           // min(MAX_NINIO, k * ninio)
+    // MFE packed (upload_mfe16) only, per loop size u: il[u] + nin[k] (k = 0..5),
+    // bulge[u], 1 x (u-1) -- the interior-loop blocks' uniform energy record
+    uint32_t ku16[32][8];
     // interior term lists (see NS_MAX); *_cnt[umax] = terms with u <= umax
     uint8_t s_n1[NS_MAX], s_n2[NS_MAX], s_kind[NS_MAX];
     float s_f[NS_MAX];       // constant factor (sigma power, bulge / 1xn length)

@@ -80,11 +80,29 @@ def scost(u, S):
     return (len(e) // S) * 3 + sum(COST[kind(u1, u - u1)] for u1 in spec) + (ngen + S - 1) // S
 
 
+# one-wave roles riding on block waves (mfe_cells.hip), in block-cost units,
+# from the stamps (tools/mfe_mc_stamps.py): finalize lane-set 0 on wave 6, q5
+# on wave 1, the qm1 column minima on wave 3, the list + records on wave 4
+ROLES4 = "6:8,1:7,3:5,4:10"
+
+
+def role_loads(S):
+    """Per-wave cost of the roles (ADX_GEN_ROLES4 overrides, "wave:cost,...").
+    Only the 4-lanes-per-cell partition uses them: it serves ~96 % of an MC
+    refold's diagonals, the other two keep equal block costs."""
+    init = [0] * NBLK
+    spec = os.environ.get("ADX_GEN_ROLES4", ROLES4) if S == 4 else ""
+    for item in filter(None, spec.split(",")):
+        w, c = item.split(":")
+        init[int(w)] = int(c)
+    return init
+
+
 def partition(S=1):
     # greedy LPT over loop sizes, largest first; ties keep small u spread out
     sizes = sorted(range(MAXLOOP + 1), key=lambda u: (-scost(u, S), -ucost(u)))
     blocks = [[] for _ in range(NBLK)]
-    load = [0] * NBLK
+    load = role_loads(S)
     for u in sizes:
         b = min(range(NBLK), key=lambda k: (load[k], len(blocks[k])))
         blocks[b].append(u)
@@ -93,6 +111,13 @@ def partition(S=1):
 
 
 ASM_CHUNK = 24   # DP reads per inline-asm batch (1 VGPR per read)
+# sliced modes whose blocks get a batched path for spans that reach every loop
+# size of the block (umax >= its largest u): the sizes' reads in batches of at
+# most FULL_READS per lane, one LDS round trip each instead of one per size
+# (4 lanes per cell: 1.013M -> 1.054M MC steps/s; larger batches spill, and
+# the 2-lanes path spills 40 VGPRs with it)
+FULL_READS = int(os.environ.get("ADX_GEN_FULL_READS", "24"))
+FULL_BATCH = tuple(int(x) for x in os.environ.get("ADX_GEN_FULL", "4").split(",") if x)
 
 
 TABK = ("i11", "i12", "i21", "i22")
@@ -142,15 +167,11 @@ def emit_group_asm(u, out):
             for u1 in spec:
                 lines.append("ds_read_u8 %%[c%d], %%[ka] offset:%d" % (u1, u1))
                 outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
-            krs = (["kr0"] if need_g else []) + (["kr1"] if u >= 2 else [])
-            if krs:
-                decl.append("        uint4 %s;" % ", ".join(krs))
+            # the loop size's energy record: uniform, scalar loads (DevScaled::ku16)
             if need_g:
-                lines.append("ds_read_b128 %%[kr0], %%[kk] offset:%d" % (32 * u))
-                outs.append('[kr0] "=&v"(kr0)')
+                decl.append("        const uint4 kr0 = kg[%d];" % (2 * u))
             if u >= 2:
-                lines.append("ds_read_b128 %%[kr1], %%[kk] offset:%d" % (32 * u + 16))
-                outs.append('[kr1] "=&v"(kr1)')
+                decl.append("        const uint4 kr1 = kg[%d];" % (2 * u + 1))
         lines.append("s_waitcnt lgkmcnt(0)")
         out.append("        {")
         out.extend(decl)
@@ -158,7 +179,7 @@ def emit_group_asm(u, out):
         for ln in lines:
             out.append('            "%s\\n"' % ln)
         out.append("            : " + ", ".join(outs))
-        out.append('            : [qa] "v"(qa), [ka] "v"(ka), [kk] "v"(U.aku)')
+        out.append('            : [qa] "v"(qa), [ka] "v"(ka)')
         out.append('            : "memory");')
         # constrained cells: shapes past the allowed unpaired runs take no part
         out.append("        if (U.mk) {")
@@ -272,15 +293,11 @@ def sliced_parts(u, S, t):
         for k in range(nk):
             lines.append("ds_read_b32 %%[w%d%s], %%[qg%s] offset:%d" % (k, t, t, 4 * S * k))
             outs.append('[w%d%s] "=&v"(w%d%s)' % (k, t, k, t))
-    krs = (["kr0" + t] if gen else []) + (["kr1" + t] if u >= 2 else [])
-    if krs:
-        decl.append("uint4 %s;" % ", ".join(krs))
+    # the loop size's energy record: uniform, scalar loads (DevScaled::ku16)
     if gen:
-        lines.append("ds_read_b128 %%[kr0%s], %%[kk] offset:%d" % (t, 32 * u))
-        outs.append('[kr0%s] "=&v"(kr0%s)' % (t, t))
+        decl.append("const uint4 kr0%s = kg[%d];" % (t, 2 * u))
     if u >= 2:
-        lines.append("ds_read_b128 %%[kr1%s], %%[kk] offset:%d" % (t, 32 * u + 16))
-        outs.append('[kr1%s] "=&v"(kr1%s)' % (t, t))
+        decl.append("const uint4 kr1%s = kg[%d];" % (t, 2 * u + 1))
     # constrained cells: shapes past the allowed unpaired runs (u1 > A or u2 > B) take no part
     post.append("if (U.mk) {")
     post.append("    const int ml = %d - C.B, mh = C.A, rr = int(C.rs >> 2);" % u)
@@ -338,6 +355,8 @@ def sliced_parts(u, S, t):
         post.append("a.g%d = pmin(a.g%d, padd(w%d%s, %s));" % (k & 1, k & 1, k, t, e))
     if pl:
         post.extend(x.strip() for x in plateau_min(pl, "gk%s[%d]" % (t, KSAT), "    "))
+    # only the address operands the batch's reads use (an unused input still holds a VGPR)
+    ins = [x for x in ins if "%%[%s]" % x.split("]")[0][1:] in "".join(lines)]
     return pre, decl, lines, outs, ins, post
 
 
@@ -349,7 +368,7 @@ def emit_sliced_batch(groups, S, out, ind):
         out.extend(ind + "    " + x for x in p[0] + p[1])
     lines = sum((p[2] for p in parts), []) + ["s_waitcnt lgkmcnt(0)"]
     outs = sum((p[3] for p in parts), [])
-    ins = sum((p[4] for p in parts), []) + ['[kk] "v"(U.aku)']
+    ins = sum((p[4] for p in parts), [])
     out.append(ind + "    asm volatile(")
     for ln in lines:
         out.append(ind + '        "%s\\n"' % ln)
@@ -369,6 +388,23 @@ def emit_block_cells_sliced(blk, S, out):
     runs the generic shapes in 1/S of the instructions.  Every slice also runs
     the special shapes (counting a shape in several slices leaves the minimum
     unchanged); the caller folds a.g0 / a.g1 across the slices."""
+    if S in FULL_BATCH:
+        # every loop size of the block fits the span: the whole block's reads in
+        # one batch (one LDS round trip, then one for the dependent code reads)
+        out.append("    if (um >= %d) {" % max(blk))
+        groups, cur, nrd = [], [], 0
+        for u in blk:   # batches of at most FULL_READS reads per lane
+            r = len(sliced_parts(u, S, "x")[2])
+            if cur and nrd + r > FULL_READS:
+                groups.append(cur)
+                cur, nrd = [], 0
+            cur.append((u, "u%d" % u))
+            nrd += r
+        groups.append(cur)
+        for g in groups:
+            emit_sliced_batch(g, S, out, "        ")
+        out.append("        goto fin;")
+        out.append("    }")
     for u in blk:
         out.append("    if (um < %d) goto fin;" % u)
         emit_sliced_batch([(u, "a")], S, out, "    ")
@@ -389,6 +425,8 @@ def main():
         out.append("    int ci = C.i, dd = U.d, um = U.umax;")
         out.append('    asm volatile("" : "+v"(ci));')
         out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
+        out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
+        out.append('    asm volatile("" : "+s"(kg));')
         emit_table_decl(blk, out)
         for u in blk:
             out.append("    if (um < %d) goto fin;" % u)
@@ -420,6 +458,8 @@ def main():
             out.append("    int ci = C.i, dd = U.d, um = U.umax, ea = C.ea, eb = C.eb;")
             out.append('    asm volatile("" : "+v"(ci), "+v"(ea), "+v"(eb));')
             out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
+            out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
+            out.append('    asm volatile("" : "+s"(kg));')
             emit_table_decl(blk, out)
             emit_block_cells_sliced(blk, S, out)
             out.append("}")
