@@ -10,8 +10,8 @@ mkdir -p $D
 export TMPDIR=/tmp
 run() {   # name, bench args
   local n=$1; shift
-  timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $D/$n/f -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $D/$n.fetch.log 2>&1
-  timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $D/$n/w -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $D/$n.write.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $D/$n/f -o f --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sub-records "$@" > $D/$n.fetch.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $D/$n/w -o w --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sub-records "$@" > $D/$n.write.log 2>&1
   python tools/pmc_traffic.py $(find $D/$n/f -name "*counter_collection.csv") $(find $D/$n/w -name "*counter_collection.csv") > $D/traffic_latest_$n.json
 }
 W=${WORKLOADS:-"mfe pf pf_bppm pf_bppm_n150"}

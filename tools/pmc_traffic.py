@@ -4,8 +4,8 @@
 
 MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are kilobytes at the L2's
 fabric side; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
-reads, so it is doubled.  Per score_kernel instantiation the first dispatch
-(walkers_init) is skipped and the rest averaged; the per-step figure sums the
+reads, so it is doubled.  Per kernel the first dispatch (walkers_init) is
+skipped and the rest averaged (a kernel only walkers_init launches is left out); the per-step figure sums the
 instantiations (the MFE step = packed 16-bit kernel + FP32 fallback launch).
 
 usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv > traffic.json
@@ -29,7 +29,9 @@ def per_kernel(path, counter):
     out = {}
     for name, disp in acc.items():
         ids = sorted(disp)
-        vals = [disp[i] for i in (ids[1:] if len(ids) > 1 else ids)]
+        if len(ids) < 2:   # launched only by walkers_init (the initial full folds): not a step kernel
+            continue
+        vals = [disp[i] for i in ids[1:]]
         out[name] = (sum(vals) / len(vals), len(vals))
     return out
 
@@ -37,9 +39,18 @@ def per_kernel(path, counter):
 def main():
     f = per_kernel(sys.argv[1], "FETCH_SIZE")
     w = per_kernel(sys.argv[2], "WRITE_SIZE")
-    kernels = {}
+    # a kernel launched in fewer than half of the steps the fold kernels ran in
+    # (the first MC step's full-fold path before any table slot is stored) is
+    # left out of the per-step figure and listed apart
+    nmax = max([n for k, (_, n) in f.items() if "combine_kernel" not in k] or [0])
+    rare = {k for k, (_, n) in f.items() if 2 * n < nmax}
+    kernels, skipped = {}, {}
     total = 0.0
     for name in sorted(set(f) | set(w)):
+        if name in rare:
+            skipped[name] = {"fetch_size_kb_raw": f[name][0], "write_size_kb": w.get(name, (0.0, 0))[0],
+                             "launches": f[name][1]}
+            continue
         fk = f.get(name, (0.0, 0))[0]
         wk = w.get(name, (0.0, 0))[0]
         b = (2.0 * fk + wk) * 1024.0
@@ -49,7 +60,7 @@ def main():
     # the kernel with the most bytes per launch (short name, as rocprof lists it)
     top = max(kernels, key=lambda k: kernels[k]["bytes"]) if kernels else ""
     short = top.replace("(anonymous namespace)::", "").replace("void ", "").replace("adx::", "").split("(")[0]
-    out = {"kernel": short, "kernels": kernels, "bytes_per_launch": total,
+    out = {"kernel": short, "kernels": kernels, "bytes_per_launch": total, "not_per_step": skipped,
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM); KB = 1024 B"}
     print(json.dumps(out, indent=1))
 
