@@ -837,15 +837,22 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         const f2 *pr = L.qm + rowb(i, N) - 5;      // qm(i, i+t-1) at +t (t >= 5)
                         f2 A = {0.f, 0.f}, A1 = {0.f, 0.f}, Pp = {0.f, 0.f};
                         float wt = L.pw[t0];                   // pw(t) = pw(t0) (expMLbase sigma)^(t - t0)
-                        for (int t = t0; t <= t1; t += 8) {
-                            f2 qv[8], rv[8];
+                        // pairs of split points per step of the loop: a read past the
+                        // lane's share is a wasted LDS cycle, and M's reads set the
+                        // step (chunks of 8: 877k, 4: 907k, 2: 922k, single points
+                        // 865k, 8 then pairs 911k MC steps/s).  Even chunks keep every
+                        // point's accumulator (A even offsets, A1 odd) and order, so
+                        // the sums are bit-identical to the 8-wide chunks'
+                        auto chunk = [&](auto cw, int t) {
+                            constexpr int C = decltype(cw)::value;
+                            f2 qv[C], rv[C];
 #pragma unroll
-                            for (int kk = 0; kk < 8; kk++) {
+                            for (int kk = 0; kk < C; kk++) {
                                 qv[kk] = pq[t + kk];
                                 rv[kk] = pr[(t + kk >= 5) ? t + kk : 5];
                             }
 #pragma unroll
-                            for (int kk = 0; kk < 8; kk++) {
+                            for (int kk = 0; kk < C; kk++) {
                                 const int tt = t + kk;
                                 const f2 q = tt <= t1 ? qv[kk] : f2{0.f, 0.f};
                                 Pp = fma2(sp2(tt <= upi ? wt : 0.f), q, Pp);
@@ -853,7 +860,8 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                                 if (kk & 1) A1 = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A1);
                                 else A = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A);
                             }
-                        }
+                        };
+                        for (int t = t0; t <= t1; t += 2) chunk(std::integral_constant<int, 2>{}, t);
                         A += A1;
                         // sum over the item's K lanes (DPP within a row of 16; the
                         // total lands in lane 0 of the item for K <= 4, lane K-1 above)

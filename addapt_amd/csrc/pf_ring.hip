@@ -43,6 +43,9 @@ namespace adx {
 namespace {
 
 constexpr int RG_NW = 14;
+#ifndef RG_MCH
+#define RG_MCH 2   // split points per M read step (even: the A / A1 split and order of 8-wide chunks)
+#endif
 constexpr int RG_NT = RG_NW * WAVE;
 constexpr int RG_NB = 7;              // interior-loop blocks (waves 0..6)
 constexpr int RG_NMW = 4;             // qm item waves
@@ -818,15 +821,17 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                         const float *pr = L.qm + rowb(i, N) - 5;
                         float A = 0.f, A1 = 0.f, Pp = 0.f;
                         float wt = L.pw[t0];
-                        for (int t = t0; t <= t1; t += 8) {
-                            float qv8[8], rv8[8];
+                        // pairs of split points per step (pf_cells.hip: reads past the
+                        // lane's share cost the LDS cycles M's chain waits on)
+                        for (int t = t0; t <= t1; t += RG_MCH) {
+                            float qv8[RG_MCH], rv8[RG_MCH];
 #pragma unroll
-                            for (int kk = 0; kk < 8; kk++) {
+                            for (int kk = 0; kk < RG_MCH; kk++) {
                                 qv8[kk] = pq[t + kk];
                                 rv8[kk] = pr[(t + kk >= 5) ? t + kk : 5];
                             }
 #pragma unroll
-                            for (int kk = 0; kk < 8; kk++) {
+                            for (int kk = 0; kk < RG_MCH; kk++) {
                                 const int tt = t + kk;
                                 const float q = tt <= t1 ? qv8[kk] : 0.f;
                                 Pp = fmaf(tt <= upi ? wt : 0.f, q, Pp);
