@@ -28,9 +28,9 @@ L.adx_debug_stamps_cells(buf, 1)
 _, _, c = eng.download()
 scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = scored * 2   # fold groups
-cols = ["setup", "F", "Bcell", "Bblock", "Bfold", "Msetup", "Mchunks", "Mtail", "Q", "barrier", "top"]
+cols = ["setup", "restore", "seq", "motif", "cells", "F", "Bcell", "Bblock", "Bfold", "Msetup", "Mchunks", "Mtail", "Q", "barrier", "top"]
 print("cycles per fold group per wave (N=%d, W=%d, %d steps, %.0f groups)" % (N, W, steps, G))
-print("wave " + " ".join("%9s" % n for n in cols))
+print("wave " + " ".join("%8s" % n for n in cols))
 for w in range(8):
-    v = [buf[w * 16 + k] // max(1, G) for k in (8, 1, 9, 10, 2, 6, 7, 3, 4, 5, 0)]
-    print("%4d " % w + " ".join("%9d" % x for x in v))
+    v = [buf[w * 16 + k] // max(1, G) for k in (8, 11, 12, 13, 14, 1, 9, 10, 2, 6, 7, 3, 4, 5, 0)]
+    print("%4d " % w + " ".join("%8d" % x for x in v))
