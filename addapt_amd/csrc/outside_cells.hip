@@ -39,6 +39,10 @@
 #include "dev_types.hpp"
 #include "fold_common.hpp"
 
+#ifndef MS_CH
+#define MS_CH 4   // terms per multiloop-sum read step (even; 16: 423k, 4: 430k, 2: 424k config-3 MC steps/s)
+#endif
+
 namespace adx {
 
 #ifdef ADX_STAMP
@@ -557,6 +561,23 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
                 if (!valid) i = N - d;
                 const int j = i + d;
                 float acc = 0.f, acc1 = 0.f;
+                // sum_t y[t] q[t] over t = ta .. tl (the lane's own bound), MS_CH terms
+                // per step: the loop ends at the lane's range, so a lane reads at most
+                // MS_CH - 1 terms past it (each a wasted LDS cycle on the chain the
+                // step waits on; pf_cells.hip qm items); even offsets into acc, odd
+                // into acc1, in order -- bit-identical to the 16-wide chunks
+                auto msum = [&](const float *py, const float *pq, int ta, int tl, float &a0, float &a1) {
+                    for (int t = ta; t <= tl; t += MS_CH) {
+                        float yv[MS_CH], qv[MS_CH];
+#pragma unroll
+                        for (int k = 0; k < MS_CH; k++) { yv[k] = py[t + k]; qv[k] = pq[t + k]; }
+#pragma unroll
+                        for (int k = 0; k < MS_CH; k += 2) {
+                            a0 = fmaf(t + k <= tl ? yv[k] : 0.f, qv[k], a0);
+                            a1 = fmaf(t + k + 1 <= tl ? yv[k + 1] : 0.f, qv[k + 1], a1);
+                        }
+                    }
+                };
                 if (isq) {
                     // qmb: t = 0 .. N-j-5: Y(i, j+5+t) = YR[rowb(i) + d + 1 + t],
                     // qm1(j+1, j+5+t) = Q1R[rowb(j+1) + t]
@@ -564,48 +585,14 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
                     const int T = N - (1 + ls * WAVE + d) - 4;          // the lane-set's longest range
                     const int ta = (T * pi) / np, tb = (T * (pi + 1)) / np;
                     const float *py = L.yr + rowb(i, N) + d + 1, *pq = L.q1r + rowb(j + 1, N);
-                    for (int t = ta; t < tb; t += 16) {
-                        float yv[16], qv[16];
-#pragma unroll
-                        for (int k = 0; k < 16; k++) { yv[k] = py[t + k]; qv[k] = pq[t + k]; }
-                        if (__ballot(lim < t + 15 || tb < t + 16) == 0) {
-#pragma unroll
-                            for (int k = 0; k < 16; k += 2) {
-                                acc = fmaf(yv[k], qv[k], acc);
-                                acc1 = fmaf(yv[k + 1], qv[k + 1], acc1);
-                            }
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < 16; k += 2) {
-                                acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, qv[k], acc);
-                                acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, qv[k + 1], acc1);
-                            }
-                        }
-                    }
+                    msum(py, pq, ta, min(lim, tb - 1), acc, acc1);
                 } else {
                     // r2: ip = 1 .. i-5: Y(ip, j) = YC[colb(j) + ip - 1], qm(ip, i-1) = QMC[colb(i-1) + ip - 1]
                     const int lim = i - 5;
                     const int T = ilast - 5;
                     const int ta = 1 + (T * pi) / np, tb = 1 + (T * (pi + 1)) / np;
                     const float *py = L.yc + colb(j) - 1, *pq = L.qmc + colb(i - 1) - 1;
-                    for (int t = ta; t < tb; t += 16) {
-                        float yv[16], qv[16];
-#pragma unroll
-                        for (int k = 0; k < 16; k++) { yv[k] = py[t + k]; qv[k] = pq[t + k]; }
-                        if (__ballot(lim < t + 15 || tb < t + 16) == 0) {
-#pragma unroll
-                            for (int k = 0; k < 16; k += 2) {
-                                acc = fmaf(yv[k], qv[k], acc);
-                                acc1 = fmaf(yv[k + 1], qv[k + 1], acc1);
-                            }
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < 16; k += 2) {
-                                acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, qv[k], acc);
-                                acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, qv[k + 1], acc1);
-                            }
-                        }
-                    }
+                    msum(py, pq, ta, min(lim, tb - 1), acc, acc1);
                 }
                 L.mlp[(par * OX_NM + mw) * WAVE + lane] = acc + acc1;
             }
