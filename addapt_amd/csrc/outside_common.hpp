@@ -170,6 +170,9 @@ struct OxSizeQ {
         }
     }
 };
+#ifndef ADX_SMALL_R0
+#define ADX_SMALL_R0 1   // sizes <= 5 on phase 0 only (the other phases' copies are discarded)
+#endif
 template <int U>
 struct OxBlk {   // the size's state in a B wave (sizes <= 5 whole in every lane)
     using T = typename std::conditional<(U <= 5), OxSize<U>, OxSizeQ<U>>::type;
@@ -181,10 +184,11 @@ __device__ __forceinline__ void ox_load(typename OxBlk<U>::T &z, const OxL &L, i
 }
 template <int U>
 __device__ __forceinline__ void ox_run(const typename OxBlk<U>::T &z, const OxL &L, const OxCell &c, int d, int umax,
-                                       int ty2, int ctb, float outer, float &g, float &sp, float &gs, float &sps) {
+                                       int ty2, int ctb, float outer, float &g, float &sp, float &gs, float &sps,
+                                       int r) {
     if constexpr (U < 0) {
     } else if constexpr (U <= 5) {
-        z.run(L, c, d, umax, ty2, gs, sps);
+        if (!ADX_SMALL_R0 || r == 0) z.run(L, c, d, umax, ty2, gs, sps);   // counted on phase 0 only
     } else {
         z.run(L, c, d, umax, ctb, outer, g, sp);
     }
@@ -252,11 +256,11 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
             const float outer = r < 2 ? c.tau_in : c.mo_in;
             float g = 0.f, sp = 0.f, gs = 0.f, sps = 0.f;
             OSTAMP(2);   // B cell setup
-            ox_run<U0>(s0, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
-            ox_run<U1>(s1, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
-            ox_run<U2>(s2, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
-            ox_run<U3>(s3, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
-            ox_run<U4>(s4, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps);
+            ox_run<U0>(s0, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps, r);
+            ox_run<U1>(s1, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps, r);
+            ox_run<U2>(s2, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps, r);
+            ox_run<U3>(s3, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps, r);
+            ox_run<U4>(s4, L, c, d, umax, ty2, ctb, outer, g, sp, gs, sps, r);
             OSTAMP(3);   // B shapes
             // small sizes count once (phase 0), then the cell's total over its four lanes
             const float part = quad_sum_f(fmaf(g, c.mmin, sp) + (r == 0 ? fmaf(gs, c.mmin, sps) : 0.f));

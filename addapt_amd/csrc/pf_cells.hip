@@ -290,6 +290,9 @@ __device__ unsigned long long g_stamps_p[16][8];
 // PxSizeQ (shapes spread over the phases), sizes <= 5 (the stack, 1x1..2x3
 // table loops) computed whole by every lane and counted once (phase 0).  The
 // four partials are summed by DPP and phase 0 writes the cell's natural slot.
+#ifndef ADX_SMALL_R0
+#define ADX_SMALL_R0 1   // sizes <= 5 on phase 0 only (the other phases' copies are discarded)
+#endif
 template <int U>
 struct PxBlk {   // the size's state in a B wave
     using T = typename std::conditional<(U < 0), PxSize<-1>, typename std::conditional<(U <= 5), PxSize<U>, PxSizeQ<U>>::type>::type;
@@ -299,7 +302,8 @@ __device__ __forceinline__ void px_run(const typename PxBlk<U>::T &z, const PxL 
                                        int r, int ctb, float outer, f2 &g, f2 &sp, f2 &gs, f2 &sps) {
     if constexpr (U < 0) {
     } else if constexpr (U <= 5) {
-        z.template run<MK>(L, c, s, umax, gs, sps);
+        // counted on phase 0 only: the other phases skip the reads (LDS cycles)
+        if (!ADX_SMALL_R0 || r == 0) z.template run<MK>(L, c, s, umax, gs, sps);
     } else {
         z.template run<MK>(L, c, s, umax, r, ctb, outer, g, sp);
     }

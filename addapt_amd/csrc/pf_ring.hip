@@ -244,12 +244,15 @@ template <int U>
 struct RgBlk {
     using T = typename std::conditional<(U < 0), RgSize<-1>, typename std::conditional<(U <= 5), RgSize<U>, RgSizeQ<U>>::type>::type;
 };
+#ifndef ADX_SMALL_R0
+#define ADX_SMALL_R0 1   // sizes <= 5 on phase 0 only (the other phases' copies are discarded)
+#endif
 template <int U, bool MK>
 __device__ __forceinline__ void rg_run(const typename RgBlk<U>::T &z, const RgL &L, const RgCell &c, int s, int umax,
                                        int r, int ctb, float outer, float &g, float &sp, float &gs, float &sps) {
     if constexpr (U < 0) {
     } else if constexpr (U <= 5) {
-        z.template run<MK>(L, c, s, umax, gs, sps);
+        if (!ADX_SMALL_R0 || r == 0) z.template run<MK>(L, c, s, umax, gs, sps);   // counted on phase 0 only
     } else {
         z.template run<MK>(L, c, s, umax, r, ctb, outer, g, sp);
     }
