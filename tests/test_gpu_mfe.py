@@ -192,6 +192,37 @@ def test_mc_trajectory_mfe(native, oracle):
         assert list(counters[w]) == ref["counters"]
 
 
+def test_mc_trajectory_mfe_n100(native, oracle):
+    """Config 2's length: every refold runs the batched 4-lane blocks on the
+    long spans (umax >= a block's largest loop size) and the constrained-cell
+    masks (the active macrostate's enforced pairs and x blocks); trajectories,
+    proposed scores and counters equal the oracle's over 60 annealing steps."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=60)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [11, 12, 13, 14, 15, 16]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=60)
+    steps = 60
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms)
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=1e-12)
+        assert ref["rc"] == 0
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        for s in range(steps):
+            if ref["outcome"][s] != 2:
+                assert _close(tr["proposed_score"][s, w], ref["proposed_score"][s]), (w, s)
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert _close(scores[w], ref["score"])
+        assert list(counters[w]) == ref["counters"]
+
+
 def test_mc_mfe_full_size_invariants(native, oracle):
     """Config 2 size (4096 walkers, N=100): counters sum to the steps, every
     final score equals the oracle's MFE score of the final sequence."""

@@ -161,6 +161,19 @@ def test_mc_trajectory_matches_oracle(native, oracle):
     _replay(oracle, native, eng, tmpl, [active], terms, therm_o, seeds, seqs, 40)
 
 
+def test_mc_trajectory_n100(native, oracle):
+    """The PF bench's length (pf_cells_kernel refolds: qm items read in pairs,
+    sizes <= 5 on phase 0): 40 annealing steps of 4 walkers equal the oracle's."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=40)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = [21, 22, 23, 24]
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=40)
+    _replay(oracle, native, eng, tmpl, [active], terms, therm_o, seeds, seqs, 40)
+
+
 def test_mc_trajectory_auto_thermostat(native, oracle):
     tmpl, active = workloads.synthetic(60)
     terms = workloads.default_objective()
