@@ -36,16 +36,19 @@ namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-constexpr int PX_NW = 14;
-constexpr int PX_NT = PX_NW * WAVE;
+#ifndef PX_NMW_CFG
+#define PX_NMW_CFG 4
+#endif
 constexpr int PX_NB = 7;              // interior-loop blocks (waves 0..6)
-constexpr int PX_NMW = 4;             // qm item waves
+constexpr int PX_NMW = PX_NMW_CFG;    // qm item waves (10 .. 10 + PX_NMW - 1)
+constexpr int PX_NW = 10 + PX_NMW;
+constexpr int PX_NT = PX_NW * WAVE;
 // Roles of waves 7-13 (seven interior-loop waves, four qm waves: the qm wave
 // with the most items sets the step at a power-of-two lane split, so a fourth
 // qm wave halves it at about half of the spans; measured +1 % over 8 + 3).
 constexpr int PX_WF = 7, PX_WQ = 8, PX_WR = 9;   // F, Q, R
 __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most items) or -1
-    return w == 10 ? 0 : w == 11 ? 1 : w == 13 ? 2 : w == 12 ? 3 : -1;
+    return w == 10 ? 0 : w == 11 ? 1 : w == 13 ? 2 : w == 12 ? 3 : (w >= 14 && w < PX_NW) ? w - 10 : -1;
 }
 constexpr int PX_NMAX = 100;
 constexpr int PX_RF = 8;              // record fields (rec_store): word, mmo, mo, m23, 1x1..2x2 factors
@@ -78,7 +81,7 @@ __device__ __forceinline__ f2 dpp_add2(f2 v) {
 
 struct PxLay {
     int C, NP;
-    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, Q5, CT, DT, PW, BY, MT, BYTES;
+    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, UC, Q5, CT, DT, PW, BY, MT, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit PxLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
@@ -92,6 +95,7 @@ struct PxLay {
         REC = o;  o += a16(size_t(2) * 2 * PX_RF * WAVE * 4 + 16); // [parity][set][field][lane]; counts
         CL = o;   o += a16(size_t(C) + size_t(NP));               // rank lists of the changed pairable cells + counts
         MLA = o;  o += a16(size_t(2) * NP * 8);                   // split part of qm, by span parity
+        UC = o;   o += a16(size_t(2) * NP * 8);                   // unpaired part U(i, j) of qm by column j, by span parity
         Q5 = o;   o += a16(size_t(NP) * 8);
         CT = o;   o += a16(size_t(CT_SIZE) * 4);
         DT = o;   o += a16(size_t(DT_HP + N + 1) * 4);
@@ -103,7 +107,7 @@ struct PxLay {
 };
 
 struct PxL {
-    f2 *qb, *qm, *q1, *part, *mla, *q5;
+    f2 *qb, *qm, *q1, *part, *mla, *uc, *q5;
     float *rec, *ct, *dt, *pw;
     int *rcnt;
     uint8_t *cc, *cl, *cn, *S, *up, *dn, *ptn, *enc, *flg, *mat;
@@ -423,6 +427,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);       // cl[off(D) + rank] = i
     L.cn = L.cl + Y.C;                                      // cn[D] = count
     L.mla = reinterpret_cast<f2 *>(smem + Y.MLA);
+    L.uc = reinterpret_cast<f2 *>(smem + Y.UC);
     L.q5 = reinterpret_cast<f2 *>(smem + Y.Q5);
     L.ct = reinterpret_cast<float *>(smem + Y.CT);
     L.dt = reinterpret_cast<float *>(smem + Y.DT);
@@ -817,8 +822,11 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 // ---------------- M: qm items of span sq = s - 2, K lanes per item (a
                 // power of two <= 16, one DPP row), split points in contiguous runs per
                 // lane, summed over the K lanes:
-                //   qm(i, jb)  = sum_t [t <= up_i] pw(t) qm1(i+t, jb) + sum_{t >= 5} qm(i, i+t-1) qm1(i+t, jb)
+                //   qm(i, jb)  = U(i, jb) + sum_{t >= 5} qm(i, i+t-1) qm1(i+t, jb)
                 //   mla(i, sq) = the split part
+                // with the unpaired part sum_t [t <= up_i] pw(t) qm1(i+t, jb) as the column
+                // recursion U(i, jb) = qm1(i, jb) + [up_i >= 1] (expMLbase sigma) U(i+1, jb)
+                // (split points t = 0..4 read no more: 894k -> 913k MC steps/s)
                 // K follows the full fold's item count N - sq, so a refold sums every
                 // item in the order a fold from scratch does (bit-identical tables)
                 const int sq = s - 2;
@@ -834,47 +842,30 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         const bool valid = item < n;
                         const int i = lo + (valid ? item : n - 1);
                         const int jb = i + sq, T = sq - 4;
-                        const int tch = (T + K) / K;          // split points per lane
-                        const int t0 = k * tch, t1 = min(T, t0 + tch - 1);
-                        const int upi = constrained ? L.up[i] : 255;
+                        // the split points t = 5..T only; the unpaired part is the
+                        // column recursion U(i, jb) = qm1(i, jb) + [up_i >= 1] (expMLbase
+                        // sigma) U(i+1, jb), U of span sq - 1 kept by the Q wave
+                        const int nb = T - 4;
+                        const int tch = nb > 0 ? (nb + K - 1) / K : 0;   // split points per lane
+                        const int t0 = 5 + k * tch, t1 = min(T, t0 + tch - 1);
                         const f2 *pq = L.q1 + colb(jb) + i - 1;   // qm1(i+t, jb) at +t
                         const f2 *pr = L.qm + rowb(i, N) - 5;      // qm(i, i+t-1) at +t (t >= 5)
-                        f2 A = {0.f, 0.f}, A1 = {0.f, 0.f}, Pp = {0.f, 0.f};
-                        float wt = L.pw[t0];                   // pw(t) = pw(t0) (expMLbase sigma)^(t - t0)
-                        // pairs of split points per step of the loop: a read past the
-                        // lane's share is a wasted LDS cycle, and M's reads set the
-                        // step (chunks of 8: 877k, 4: 907k, 2: 922k, single points
-                        // 865k, 8 then pairs 911k MC steps/s).  Even chunks keep every
-                        // point's accumulator (A even offsets, A1 odd) and order, so
-                        // the sums are bit-identical to the 8-wide chunks'
-                        auto chunk = [&](auto cw, int t) {
-                            constexpr int C = decltype(cw)::value;
-                            f2 qv[C], rv[C];
-#pragma unroll
-                            for (int kk = 0; kk < C; kk++) {
-                                qv[kk] = pq[t + kk];
-                                rv[kk] = pr[(t + kk >= 5) ? t + kk : 5];
-                            }
-#pragma unroll
-                            for (int kk = 0; kk < C; kk++) {
-                                const int tt = t + kk;
-                                const f2 q = tt <= t1 ? qv[kk] : f2{0.f, 0.f};
-                                Pp = fma2(sp2(tt <= upi ? wt : 0.f), q, Pp);
-                                wt *= mlbase_sig;
-                                if (kk & 1) A1 = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A1);
-                                else A = fma2(tt >= 5 ? rv[kk] : f2{0.f, 0.f}, q, A);
-                            }
-                        };
-                        for (int t = t0; t <= t1; t += 2) chunk(std::integral_constant<int, 2>{}, t);
+                        const bool up1 = sq >= 5 && (!constrained || L.up[i] >= 1);
+                        const f2 u1 = up1 ? L.uc[((sq - 1) & 1) * NP + jb] : f2{0.f, 0.f};
+                        const f2 q0 = pq[0];
+                        f2 A = {0.f, 0.f}, A1 = {0.f, 0.f};
+                        for (int t = t0; t <= t1; t += 2) {   // pairs: even offsets in A, odd in A1
+                            const f2 qa = pq[t], qn = pq[t + 1], ra = pr[t], rn = pr[t + 1];
+                            A = fma2(ra, qa, A);
+                            A1 = fma2(rn, t + 1 <= t1 ? qn : f2{0.f, 0.f}, A1);
+                        }
                         A += A1;
-                        // sum over the item's K lanes (DPP within a row of 16; the
-                        // total lands in lane 0 of the item for K <= 4, lane K-1 above)
-                        if (K >= 2) { A = dpp_add2<0xb1>(A); Pp = dpp_add2<0xb1>(Pp); }     // quad_perm [1,0,3,2]
-                        if (K >= 4) { A = dpp_add2<0x4e>(A); Pp = dpp_add2<0x4e>(Pp); }     // quad_perm [2,3,0,1]
-                        if (K >= 8) { A = dpp_add2<0x114>(A); Pp = dpp_add2<0x114>(Pp); }   // row_shr:4
-                        if (K >= 16) { A = dpp_add2<0x118>(A); Pp = dpp_add2<0x118>(Pp); }  // row_shr:8
+                        if (K >= 2) A = dpp_add2<0xb1>(A);     // quad_perm [1,0,3,2]
+                        if (K >= 4) A = dpp_add2<0x4e>(A);     // quad_perm [2,3,0,1]
+                        if (K >= 8) A = dpp_add2<0x114>(A);    // row_shr:4
+                        if (K >= 16) A = dpp_add2<0x118>(A);   // row_shr:8
                         if (valid && k == (K >= 8 ? K - 1 : 0)) {
-                            L.qm[rowb(i, N) + sq - 4] = A + Pp;
+                            L.qm[rowb(i, N) + sq - 4] = A + fma2(sp2(mlbase_sig), u1, q0);
                             L.mla[(sq & 1) * NP + i] = A;
                         }
                     }
@@ -928,6 +919,17 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     }
                     acc = wave_sum_f2(acc);
                     if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sp2(sig1) : f2{0.f, 0.f}) + acc;
+                }
+                {   // U(i, jb) of span sq = s - 2 for every cell (M reads it next step)
+                    const int sq = s - 2;
+                    if (sq >= 4 && sq <= N - 4) {
+                        for (int i = 1 + lane; i <= N - sq; i += WAVE) {
+                            const int jb = i + sq;
+                            const bool up1 = sq >= 5 && (!constrained || L.up[i] >= 1);
+                            const f2 u1 = up1 ? L.uc[((sq - 1) & 1) * NP + jb] : f2{0.f, 0.f};
+                            L.uc[(sq & 1) * NP + jb] = fma2(sp2(mlbase_sig), u1, L.q1[colb(jb) + i - 1]);
+                        }
+                    }
                 }
                 qfac(j + 1);
             } else if (wid == PX_WR) {
