@@ -43,9 +43,6 @@ namespace adx {
 namespace {
 
 constexpr int RG_NW = 14;
-#ifndef RG_MCH
-#define RG_MCH 2   // split points per M read step (even: the A / A1 split and order of 8-wide chunks)
-#endif
 constexpr int RG_NT = RG_NW * WAVE;
 constexpr int RG_NB = 7;              // interior-loop blocks (waves 0..6)
 constexpr int RG_NMW = 4;             // qm item waves
@@ -62,7 +59,7 @@ constexpr int RG_SLACK = 16;
 
 struct RgLay {
     int C, NP, RS;
-    size_t QM, Q1, QB, CC, PART, REC, CL, MLA, Q5, CT, DT, PW, BY, MT, BYTES;
+    size_t QM, Q1, QB, CC, PART, REC, CL, MLA, UC, Q5, CT, DT, PW, BY, MT, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit RgLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
@@ -77,6 +74,7 @@ struct RgLay {
         REC = o;  o += a16(size_t(2) * RG_SETS * RG_RF * WAVE * 4 + 16);   // [parity][set][field][lane]; counts
         CL = o;   o += a16(size_t(C) + size_t(NP));               // rank lists of the changed pairable cells + counts
         MLA = o;  o += a16(size_t(2) * NP * 4);                   // split part of qm, by span parity
+        UC = o;   o += a16(size_t(2) * NP * 4);                   // unpaired part U(i, j) of qm by column j, by span parity
         Q5 = o;   o += a16(size_t(NP) * 4);
         CT = o;   o += a16(size_t(CT_SIZE) * 4);
         DT = o;   o += a16(size_t(DT_HP + N + 1) * 4);
@@ -88,7 +86,7 @@ struct RgLay {
 };
 
 struct RgL {
-    float *qm, *q1, *qb, *part, *mla, *q5, *rec, *ct, *dt, *pw;
+    float *qm, *q1, *qb, *part, *mla, *uc, *q5, *rec, *ct, *dt, *pw;
     int *rcnt;
     uint8_t *cc, *cl, *cn, *S, *up, *dn, *ptn, *enc, *flg, *mat;
     int N, NP, RS;
@@ -404,6 +402,7 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);
     L.cn = L.cl + Y.C;
     L.mla = reinterpret_cast<float *>(smem + Y.MLA);
+    L.uc = reinterpret_cast<float *>(smem + Y.UC);
     L.q5 = reinterpret_cast<float *>(smem + Y.Q5);
     L.ct = reinterpret_cast<float *>(smem + Y.CT);
     L.dt = reinterpret_cast<float *>(smem + Y.DT);
@@ -817,39 +816,30 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                         const bool valid = item < n;
                         const int i = lo + (valid ? item : n - 1);
                         const int jb = i + sq, T = sq - 4;
-                        const int tch = (T + K) / K;
-                        const int t0 = k * tch, t1 = min(T, t0 + tch - 1);
-                        const int upi = constrained ? L.up[i] : 255;
+                        // split points t = 5..T; the unpaired part is the column recursion
+                        // U(i, jb) = qm1(i, jb) + [up_i >= 1] (expMLbase sigma) U(i+1, jb),
+                        // U of span sq - 1 kept by the Q wave (pf_cells.hip)
+                        const int nb = T - 4;
+                        const int tch = nb > 0 ? (nb + K - 1) / K : 0;
+                        const int t0 = 5 + k * tch, t1 = min(T, t0 + tch - 1);
                         const float *pq = L.q1 + colb(jb) + i - 1;
                         const float *pr = L.qm + rowb(i, N) - 5;
-                        float A = 0.f, A1 = 0.f, Pp = 0.f;
-                        float wt = L.pw[t0];
-                        // pairs of split points per step (pf_cells.hip: reads past the
-                        // lane's share cost the LDS cycles M's chain waits on)
-                        for (int t = t0; t <= t1; t += RG_MCH) {
-                            float qv8[RG_MCH], rv8[RG_MCH];
-#pragma unroll
-                            for (int kk = 0; kk < RG_MCH; kk++) {
-                                qv8[kk] = pq[t + kk];
-                                rv8[kk] = pr[(t + kk >= 5) ? t + kk : 5];
-                            }
-#pragma unroll
-                            for (int kk = 0; kk < RG_MCH; kk++) {
-                                const int tt = t + kk;
-                                const float q = tt <= t1 ? qv8[kk] : 0.f;
-                                Pp = fmaf(tt <= upi ? wt : 0.f, q, Pp);
-                                wt *= mlbase_sig;
-                                if (kk & 1) A1 = fmaf(tt >= 5 ? rv8[kk] : 0.f, q, A1);
-                                else A = fmaf(tt >= 5 ? rv8[kk] : 0.f, q, A);
-                            }
+                        const bool up1 = sq >= 5 && (!constrained || L.up[i] >= 1);
+                        const float u1 = up1 ? L.uc[((sq - 1) & 1) * NP + jb] : 0.f;
+                        const float q0 = pq[0];
+                        float A = 0.f, A1 = 0.f;
+                        for (int t = t0; t <= t1; t += 2) {   // pairs: even offsets in A, odd in A1
+                            const float qa = pq[t], qn = pq[t + 1], ra = pr[t], rn = pr[t + 1];
+                            A = fmaf(ra, qa, A);
+                            A1 = fmaf(rn, t + 1 <= t1 ? qn : 0.f, A1);
                         }
                         A += A1;
-                        if (K >= 2) { A = dpp_add<0xb1>(A); Pp = dpp_add<0xb1>(Pp); }
-                        if (K >= 4) { A = dpp_add<0x4e>(A); Pp = dpp_add<0x4e>(Pp); }
-                        if (K >= 8) { A = dpp_add<0x114>(A); Pp = dpp_add<0x114>(Pp); }
-                        if (K >= 16) { A = dpp_add<0x118>(A); Pp = dpp_add<0x118>(Pp); }
+                        if (K >= 2) A = dpp_add<0xb1>(A);
+                        if (K >= 4) A = dpp_add<0x4e>(A);
+                        if (K >= 8) A = dpp_add<0x114>(A);
+                        if (K >= 16) A = dpp_add<0x118>(A);
                         if (valid && k == (K >= 8 ? K - 1 : 0)) {
-                            L.qm[rowb(i, N) + sq - 4] = A + Pp;
+                            L.qm[rowb(i, N) + sq - 4] = A + fmaf(mlbase_sig, u1, q0);
                             L.mla[(sq & 1) * NP + i] = A;
                         }
                     }
@@ -920,6 +910,17 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                     if (lane == 0) L.q5[j] = (L.up[j] >= 1 ? L.q5[j - 1] * sig1 : 0.f) + acc;
                 }
                 RSTAMP(5);         // q5
+                {   // U(i, jb) of span sq = s - 2 for every cell (M reads it next step)
+                    const int sq = s - 2;
+                    if (sq >= 4 && sq <= N - 4) {
+                        for (int i = 1 + lane; i <= N - sq; i += WAVE) {
+                            const int jb = i + sq;
+                            const bool up1 = sq >= 5 && (!constrained || L.up[i] >= 1);
+                            const float u1 = up1 ? L.uc[((sq - 1) & 1) * NP + jb] : 0.f;
+                            L.uc[(sq & 1) * NP + jb] = fmaf(mlbase_sig, u1, L.q1[colb(jb) + i - 1]);
+                        }
+                    }
+                }
                 // column s - 2 is final: its last cell, (1, s-2), was finalised two steps
                 // ago and its store drained by F at the start of the last step
                 qload(s - 2);
