@@ -122,6 +122,36 @@ FULL_BATCH = tuple(int(x) for x in os.environ.get("ADX_GEN_FULL", "4").split(","
 
 TABK = ("i11", "i12", "i21", "i22")
 
+# 4 lanes per cell: generic shapes whose energies differ between the slices of a
+# read row k (|2 u1 - u| < KSAT for some slice) take them from a per-lane LDS
+# table (mfe_cells.hip CL::e4, slot q at byte 16 q + 4 r for slice r) read in the
+# batch, instead of a per-lane select among the record's scalar values
+ETAB4 = os.environ.get("ADX_GEN_ETAB4", "1") == "1"
+
+
+def gen_rows(u, S):
+    """Per read row k of loop size u with S slices: the asymmetry index
+    min(|2 u1 - u|, KSAT) of each slice (None past the generic shapes)."""
+    gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
+    if not gen:
+        return []
+    nk = (len(gen) + S - 1) // S
+    return [[min(abs(2 * u1 - u), KSAT) if u1 in gen else None
+             for u1 in (gen[0] + r + S * k for r in range(S))] for k in range(nk)]
+
+
+def e4_slots():
+    """(u, k, asym per slice) of every 4-slice row with differing energies."""
+    out = []
+    for u in range(MAXLOOP + 1):
+        for k, row in enumerate(gen_rows(u, 4)):
+            if len(set(row)) > 1:
+                out.append((u, k, row))
+    return out
+
+
+E4_SLOT = {(u, k): q for q, (u, k, _) in enumerate(e4_slots())}
+
 
 def plateau_min(vals, e, ind):
     """Generic shapes with the saturated (plateau) energy e: a pairwise min tree,
@@ -293,6 +323,16 @@ def sliced_parts(u, S, t):
         for k in range(nk):
             lines.append("ds_read_b32 %%[w%d%s], %%[qg%s] offset:%d" % (k, t, t, 4 * S * k))
             outs.append('[w%d%s] "=&v"(w%d%s)' % (k, t, k, t))
+    etab = []   # rows k whose energies come from the per-lane table
+    if ETAB4 and S == 4:
+        for k in range(nk):
+            if (u, k) in E4_SLOT:
+                etab.append(k)
+                decl.append("uint32_t e%d%s;" % (k, t))
+                lines.append("ds_read_b32 %%[e%d%s], %%[qt%s] offset:%d" % (k, t, t, 16 * E4_SLOT[(u, k)]))
+                outs.append('[e%d%s] "=&v"(e%d%s)' % (k, t, k, t))
+        if etab:
+            ins.append('[qt%s] "v"(C.ee)' % t)
     # the loop size's energy record: uniform, scalar loads (DevScaled::ku16)
     if gen:
         decl.append("const uint4 kr0%s = kg[%d];" % (t, 2 * u))
@@ -348,6 +388,8 @@ def sliced_parts(u, S, t):
             continue
         if len(set(vals)) == 1:
             e = vals[0]
+        elif k in etab:
+            e = "e%d%s" % (k, t)
         elif S == 2:
             e = "(C.r1 ? %s : %s)" % (vals[1], vals[0])
         else:
@@ -480,6 +522,13 @@ def main():
                 tb |= 1 << b
         out.append("constexpr unsigned MFE_TABLE_BLOCKS%s = 0x%xu;   // blocks with 1x1 / 1x2 / 2x1 / 2x2 shapes%s"
                    % ("" if S == 1 else "_S%d" % S, tb, "" if S == 1 else " (%d lanes per cell)" % S))
+    sl = e4_slots() if ETAB4 else []
+    out.append("// per-lane generic energies of the 4-lanes-per-cell blocks: slot q holds loop size")
+    out.append("// MFE_E4_U[q] and, for slice r, the Ninio index MFE_E4_A[q][r] (-1: no shape)")
+    out.append("constexpr int MFE_E4_SLOTS = %d;" % len(sl))
+    out.append("constexpr signed char MFE_E4_U[%d] = {%s};" % (max(1, len(sl)), ", ".join(str(u) for u, _, _ in sl) or "0"))
+    out.append("constexpr signed char MFE_E4_A[%d][4] = {%s};" % (max(1, len(sl)), ", ".join(
+        "{%s}" % ", ".join(str(-1 if a is None else a) for a in row) for _, _, row in sl) or "{-1, -1, -1, -1}"))
     out.append("constexpr int MFE_NBLK = %d;" % NBLK)
     out.append("constexpr int MFE_KSAT = %d;   // generic loops: nin[k] == nin[MFE_KSAT] for k >= MFE_KSAT" % KSAT)
     path = os.path.join(out_dir(), "mfe_blocks.inc")
