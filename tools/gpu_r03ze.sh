@@ -5,7 +5,7 @@ D=gpurun_out/r03ze
 mkdir -p $D
 export TMPDIR=/tmp
 for k in 1 2; do
-for v in et spec; do
+for v in et spec mfe_lw7 mfe_lw7s; do
 ADX_LIB=addapt_amd/_lib/ablate/lib_$v.so timeout -k 10 200 python bench.py --steps 100 --no-cpu-baseline --no-sub-records > $D/mfe_${v}_$k.json 2> $D/mfe_${v}_$k.err
 done
 done
