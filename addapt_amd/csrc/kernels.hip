@@ -1727,6 +1727,103 @@ __device__ double mt_canonical(MtView &g, int lane) {
     return ret;
 }
 
+// ---------------------------------------------------------------- median
+// std::nth_element(a, a + k, a + n) over doubles with operator<, following
+// libstdc++ 11's introselect (<bits/stl_algo.h> __introselect,
+// __unguarded_partition_pivot, __move_median_to_first, __insertion_sort;
+// <bits/stl_heap.h> __heap_select / __adjust_heap / __push_heap) compare for
+// compare and swap for swap.  AutoScalingThermostat::adjust calls it on its
+// training set (sampling.cc:389-393); keeping the same order of operations
+// puts the same element at k even among +0.0 / -0.0 ties and NaNs.  Run by one
+// lane on the walker's training buffer (<= period doubles, once per period).
+__device__ __forceinline__ void nth_swap(double *a, int i, int j) {
+    const double t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+}
+
+__device__ void nth_adjust_heap(double *a, int hole, int len, double v) {
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (a[child] < a[child - 1]) child--;
+        a[hole] = a[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        a[hole] = a[child - 1];
+        hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && a[parent] < v) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = v;
+}
+
+__device__ void nth_element_libstdcxx(double *a, int k, int n) {
+    if (n == 0 || k == n) return;
+    int first = 0, last = n;
+    int depth = 2 * (31 - __clz(n));
+    while (last - first > 3) {
+        if (depth == 0) {
+            // __heap_select(first, k + 1, last) then iter_swap(first, k)
+            double *h = a + first;
+            const int mid = k + 1 - first, len = last - first;
+            if (mid >= 2)
+                for (int p = (mid - 2) / 2;; p--) {
+                    nth_adjust_heap(h, p, mid, h[p]);
+                    if (p == 0) break;
+                }
+            for (int i = mid; i < len; i++)
+                if (h[i] < h[0]) {
+                    const double v = h[i];
+                    h[i] = h[0];
+                    nth_adjust_heap(h, 0, mid, v);
+                }
+            nth_swap(a, first, k);
+            return;
+        }
+        --depth;
+        // __unguarded_partition_pivot: median of (first+1, mid, last-1) to first
+        const int m = first + (last - first) / 2, x = first + 1, z = last - 1;
+        int pick;
+        if (a[x] < a[m]) pick = (a[m] < a[z]) ? m : (a[x] < a[z]) ? z : x;
+        else pick = (a[x] < a[z]) ? x : (a[m] < a[z]) ? z : m;
+        nth_swap(a, first, pick);
+        int lo = first + 1, hi = last;
+        for (;;) {
+            while (a[lo] < a[first]) lo++;
+            hi--;
+            while (a[first] < a[hi]) hi--;
+            if (!(lo < hi)) break;
+            nth_swap(a, lo, hi);
+            lo++;
+        }
+        if (lo <= k) first = lo;
+        else last = lo;
+    }
+    // __insertion_sort(first, last)
+    for (int i = first + 1; i < last; i++) {
+        const double v = a[i];
+        if (v < a[first]) {
+            for (int j = i; j > first; j--) a[j] = a[j - 1];
+            a[first] = v;
+        } else {
+            int hole = i;
+            while (v < a[hole - 1]) {
+                a[hole] = a[hole - 1];
+                hole--;
+            }
+            a[hole] = v;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- MC step
 // One MonteCarlo::apply iteration (sampling.cc:55-99) = three launches on one
 // stream: propose_kernel (thermostat, RNG streams, mutation move, unchanged
@@ -1755,37 +1852,25 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
     } else {
         double *tr = st.train + size_t(w) * st.period;
         const int n = st.ntrain[w] + 1;
-        if (lane == 0) tr[n - 1] = st.last_diff[w];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
         T = st.auto_T[w];
-        if (n >= st.period) {
-            // nth_element(n/2): a value whose rank window covers n/2
-            const int k = n / 2;
-            double found = 0.0;
-            bool have = false;
-            for (int e = lane; e < n; e += WAVE) {
-                const double x = tr[e];
-                int less = 0, eq = 0;
-                for (int f = 0; f < n; f++) {
-                    const double y = tr[f];
-                    less += (y < x);
-                    eq += (y == x);
-                }
-                if (less <= k && k < less + eq) { found = x; have = true; }
-            }
-            const unsigned long long m = __ballot(have);
-            const int src = m ? __ffsll((long long)m) - 1 : 0;
-            const double med = __shfl(found, src, WAVE);
-            const double t = med / log(st.target_rate);
-            T = t > 0.0 ? t : 0.0;
-            if (lane == 0) {
-                st.auto_T[w] = T;
+        double Tn = T;
+        if (lane == 0) {
+            tr[n - 1] = st.last_diff[w];
+            if (n >= st.period) {
+                // median = std::nth_element at n/2, clamp = std::max(t, 0.0)
+                // (sampling.cc:389-396): the libstdc++ selection, so -0.0 / NaN
+                // land exactly where the reference's do
+                const int k = n / 2;
+                nth_element_libstdcxx(tr, k, n);
+                const double t = tr[k] / log(st.target_rate);
+                Tn = (t < 0.0) ? 0.0 : t;
+                st.auto_T[w] = Tn;
                 st.ntrain[w] = 0;
+            } else {
+                st.ntrain[w] = n;
             }
-        } else if (lane == 0) {
-            st.ntrain[w] = n;
         }
+        T = __shfl(Tn, 0, WAVE);
     }
     // ---- move: stream A (and C if the step will be scored)
     uint32_t *mA = mt, *mC = mt + MT_WORDS;

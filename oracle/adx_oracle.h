@@ -125,6 +125,10 @@ uint32_t orc_mt_next(orc_mt *g);
 int orc_uniform_int(orc_mt *g, int a, int b);
 /* std::uniform_real_distribution<double>(0,1)(g) = generate_canonical<double,53> */
 double orc_canonical(orc_mt *g);
+/* std::nth_element (libstdc++ 11 introselect, step for step) and the
+ * std::max(t, 0.0) clamp of AutoScalingThermostat (sampling.cc:389-396). */
+void orc_nth_element(double *a, long k, long n);
+double orc_auto_clamp(double t);
 
 /* ---- mutation move ---------------------------------------------------- */
 /* Device = sequence + M macrostates (each N chars).  Error codes: */

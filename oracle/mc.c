@@ -209,10 +209,124 @@ double orc_score(const orc_scorefxn *sf, const char *seq, int n, const char *con
 }
 
 /* ------------------------------------------------------ Monte Carlo */
-static int cmp_double(const void *a, const void *b) {
-    double x = *(const double *)a, y = *(const double *)b;
-    return (x > y) - (x < y);
+/* std::nth_element(first, first + k, first + n) over doubles with operator<,
+ * restated from libstdc++ 11 (the toolchain SURVEY §8 A11 pins):
+ * <bits/stl_algo.h> __introselect / __unguarded_partition_pivot /
+ * __move_median_to_first / __insertion_sort and <bits/stl_heap.h>
+ * __heap_select / __make_heap / __adjust_heap / __push_heap.  The order of
+ * comparisons and swaps is kept step for step, so the element that lands at
+ * position k is the one libstdc++ selects even among equal keys (+0.0 vs -0.0)
+ * and with NaNs (which make '<' no strict weak order).  The reference calls
+ * it from AutoScalingThermostat::adjust (sampling.cc:389-393). */
+static void nth_swap(double *a, long i, long j) { double t = a[i]; a[i] = a[j]; a[j] = t; }
+
+static void nth_push_heap(double *a, long hole, long top, double v) {
+    long parent = (hole - 1) / 2;
+    while (hole > top && a[parent] < v) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = v;
 }
+
+static void nth_adjust_heap(double *a, long hole, long len, double v) {
+    const long top = hole;
+    long child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (a[child] < a[child - 1]) child--;
+        a[hole] = a[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        a[hole] = a[child - 1];
+        hole = child - 1;
+    }
+    nth_push_heap(a, hole, top, v);
+}
+
+static void nth_heap_select(double *a, long mid, long last) {
+    if (mid >= 2)
+        for (long parent = (mid - 2) / 2;; parent--) {
+            nth_adjust_heap(a, parent, mid, a[parent]);
+            if (parent == 0) break;
+        }
+    for (long i = mid; i < last; i++)
+        if (a[i] < a[0]) {
+            double v = a[i];
+            a[i] = a[0];
+            nth_adjust_heap(a, 0, mid, v);
+        }
+}
+
+static void nth_insertion_sort(double *a, long first, long last) {
+    if (first == last) return;
+    for (long i = first + 1; i != last; i++) {
+        double v = a[i];
+        if (v < a[first]) {
+            memmove(a + first + 1, a + first, sizeof(double) * (size_t)(i - first));
+            a[first] = v;
+        } else {
+            long hole = i, prev = i - 1;
+            while (v < a[prev]) {
+                a[hole] = a[prev];
+                hole = prev;
+                prev--;
+            }
+            a[hole] = v;
+        }
+    }
+}
+
+static void nth_median_to_first(double *x, long r, long a, long b, long c) {
+    if (x[a] < x[b]) {
+        if (x[b] < x[c]) nth_swap(x, r, b);
+        else if (x[a] < x[c]) nth_swap(x, r, c);
+        else nth_swap(x, r, a);
+    } else if (x[a] < x[c]) nth_swap(x, r, a);
+    else if (x[b] < x[c]) nth_swap(x, r, c);
+    else nth_swap(x, r, b);
+}
+
+static long nth_partition_pivot(double *a, long first, long last) {
+    long mid = first + (last - first) / 2;
+    nth_median_to_first(a, first, first + 1, mid, last - 1);
+    long lo = first + 1, hi = last;
+    const long pivot = first;
+    for (;;) {
+        while (a[lo] < a[pivot]) lo++;
+        hi--;
+        while (a[pivot] < a[hi]) hi--;
+        if (!(lo < hi)) return lo;
+        nth_swap(a, lo, hi);
+        lo++;
+    }
+}
+
+void orc_nth_element(double *a, long k, long n) {
+    if (n == 0 || k == n) return;
+    long first = 0, last = n;
+    int lg = 63 - __builtin_clzll((unsigned long long)n);
+    long depth = 2L * lg;
+    while (last - first > 3) {
+        if (depth == 0) {
+            nth_heap_select(a + first, k + 1 - first, last - first);
+            nth_swap(a, first, k);
+            return;
+        }
+        --depth;
+        long cut = nth_partition_pivot(a, first, last);
+        if (cut <= k) first = cut;
+        else last = cut;
+    }
+    nth_insertion_sort(a, first, last);
+}
+
+/* std::max(t, 0.0) = (t < 0.0) ? 0.0 : t  (<bits/stl_algobase.h>): keeps -0.0
+ * and NaN, as AutoScalingThermostat::adjust does (sampling.cc:395-396). */
+double orc_auto_clamp(double t) { return (t < 0.0) ? 0.0 : t; }
 
 int orc_mc_run(const orc_scorefxn *sf, char *seq, int n, const char *const *ms, int nm,
                const orc_thermostat *th, uint32_t seed, int num_steps, double *final_score,
@@ -248,9 +362,8 @@ int orc_mc_run(const orc_scorefxn *sf, char *seq, int n, const char *const *ms, 
             training[ntrain++] = score_diff;
             if ((unsigned)ntrain >= (unsigned)th->period) {
                 int k = ntrain / 2;
-                qsort(training, ntrain, sizeof(double), cmp_double);
-                double t = training[k] / log(th->target_rate);
-                auto_T = t > 0.0 ? t : 0.0;
+                orc_nth_element(training, k, ntrain);
+                auto_T = orc_auto_clamp(training[k] / log(th->target_rate));
                 ntrain = 0;
             }
             temperature = auto_T;

@@ -98,6 +98,10 @@ def lib():
         L.orc_uniform_int.argtypes = [C.POINTER(MT), C.c_int, C.c_int]
         L.orc_canonical.restype = C.c_double
         L.orc_canonical.argtypes = [C.POINTER(MT)]
+        L.orc_nth_element.restype = None
+        L.orc_nth_element.argtypes = [C.POINTER(C.c_double), C.c_long, C.c_long]
+        L.orc_auto_clamp.restype = C.c_double
+        L.orc_auto_clamp.argtypes = [C.c_double]
         L.orc_mutate_recursively.restype = C.c_int
         L.orc_mutate_recursively.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.c_int,
                                              C.c_int, C.c_char]
@@ -225,6 +229,19 @@ class Rng:
 
     def canonical(self):
         return lib().orc_canonical(C.byref(self.s))
+
+
+def nth_element(values, k):
+    """std::nth_element(v, v + k, v + n) as libstdc++ 11 runs it; returns the
+    rearranged list (the reference's median step, sampling.cc:389-393)."""
+    a = (C.c_double * len(values))(*values)
+    lib().orc_nth_element(a, k, len(values))
+    return list(a)
+
+
+def auto_clamp(t):
+    """std::max(t, 0.0) (sampling.cc:395-396): -0.0 and NaN pass through."""
+    return lib().orc_auto_clamp(t)
 
 
 def mutate_recursively(seq, macrostates, pos, base):

@@ -373,3 +373,40 @@ def test_mfe_kernels_score_and_trajectory(native, oracle, monkeypatch, kernel):
         assert list(tr["outcome"][:, w]) == ref["outcome"], (kernel, w)
         assert final[w].upper() == ref["seq"].upper(), (kernel, w)
         assert list(counters[w]) == ref["counters"], (kernel, w)
+
+
+def test_mc_trajectory_mfe_auto_zero_median(native, oracle):
+    """AutoScalingThermostat in MFE mode (sampling.cc:382-401): mutations that
+    change no MFE give score differences of exactly 0.0, so medians of 0 are
+    common and T = std::max(0.0 / ln 0.5, 0.0) = -0.0.  The device's median
+    (libstdc++ nth_element restated) and clamp must reproduce the oracle's
+    temperatures bit for bit -- sign of zero included -- and with them every
+    outcome (improvements rejected, worsenings accepted under T = -0.0)."""
+    tmpl, active = workloads.synthetic(60)
+    terms = workloads.default_objective()
+    th = native.make_thermostat("auto", rate=0.5, period=4, t0=2.0)
+    eng = _engine(native, tmpl, [active], terms, thermostat=th)
+    seeds = list(range(30, 42))
+    seqs = workloads.walker_sequences(tmpl, [active], len(seeds))
+    therm_o = oracle.thermostat("auto", rate=0.5, period=4, t0=2.0)
+    steps = 80
+    eng.walkers_init(seeds, seqs)
+    tr = eng.run_steps(steps, trace=True)
+    final, scores, counters = eng.download()
+    sf = _oracle_sf(oracle, terms)
+    neg_zero = 0
+    for w, seed in enumerate(seeds):
+        forced = [int(x) for x in tr["outcome"][:, w]]
+        ref = oracle.mc_run(sf, seqs[w], [active], therm_o, seed, steps, forced=forced, tie_eps=1e-12)
+        assert ref["rc"] == 0
+        for s in range(steps):
+            a, b = tr["temperature"][s, w], ref["temperature"][s]
+            assert (math.isnan(a) and math.isnan(b)) or (a == b and math.copysign(1, a) == math.copysign(1, b)), (w, s, a, b)
+            if b == 0.0 and math.copysign(1, b) < 0:
+                neg_zero += 1
+        assert list(tr["position"][:, w]) == ref["pos"], w
+        assert list(tr["outcome"][:, w]) == ref["outcome"], w
+        assert final[w].upper() == ref["seq"].upper(), w
+        assert _close(scores[w], ref["score"])
+        assert list(counters[w]) == ref["counters"]
+    assert neg_zero > 0

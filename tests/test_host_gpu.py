@@ -193,3 +193,40 @@ def test_config1_cli_10k_steps_matches_golden(tmp_path):
             pytest.skip("near tie at step %d (margin %.2e <= %.2e): %d steps bit-exact" % (s, m, bound, s))
         prev = r["current_seq"]
     assert prev == g["final_seq"]
+
+
+@pytest.mark.gpu
+def test_cli_auto_thermostat_engine_equals_reference_loop(oracle, tmp_path):
+    """MonteCarlo::apply(device, seed) (fused engine) and apply(device, rng)
+    (the reference loop, std::nth_element + std::max in host C++) on an
+    auto-scaling thermostat with period 2: the training set [0.0, diff] has
+    median 0.0 whenever diff < 0, so T = std::max(-0.0, 0.0) = -0.0 half the
+    time (sampling.cc:389-396).  Both paths and the oracle print the same
+    temperatures (sign of zero included), outcomes and sequences."""
+    p = tmp_path / "auto.yml"
+    p.write_text(CONFIG.format(seq=workloads.RHF6_SEQ, act=workloads.RHF6_ACTIVE)
+                 .replace("thermostat: 5 to 0 in 300 steps", "thermostat: auto 50% 2 1.5"))
+    a, b = str(tmp_path / "engine.tsv"), str(tmp_path / "loop.tsv")
+    steps = 40
+    _run([str(p), "-n", str(steps), "-r", "0", "-o", a])
+    _run([str(p), "-n", str(steps), "-r", "0", "-o", b, "--reference-loop"])
+    _, ra = _read_tsv(a)
+    _, rb = _read_tsv(b)
+    assert [r["temperature"] for r in ra] == [r["temperature"] for r in rb]
+    assert [r["outcome"] for r in ra] == [r["outcome"] for r in rb]
+    assert [r["current_seq"] for r in ra] == [r["current_seq"] for r in rb]
+    assert any(r["temperature"] == "-0" for r in ra)
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
+    sf = oracle.ScoreFunction(workloads.default_objective(), aptamer=motif)
+    th = oracle.thermostat("auto", rate=0.5, period=2, t0=1.5)
+    outc = [OUTC[r["outcome"]] for r in ra]
+    ref = oracle.mc_run(sf, workloads.RHF6_SEQ, [workloads.RHF6_ACTIVE], th, 0, steps, forced=outc,
+                        tie_eps=1e-6, want_seqs=True)
+    assert outc == ref["outcome"]
+    for s, r in enumerate(ra):
+        T = ref["temperature"][s]
+        if T == 0.0:
+            assert r["temperature"] == ("-0" if math.copysign(1, T) < 0 else "0"), s
+        else:
+            assert float(r["temperature"]) == pytest.approx(T, rel=1e-5)
+        assert r["current_seq"] == ref["seqs"][s], s
