@@ -1263,7 +1263,7 @@ extern "C" adx_status adx_run_steps(adx_ctx *c, int steps, adx_trace *trace) {
     st.t_hi = c->thermo.t_hi;
     st.t_lo = c->thermo.t_lo;
     st.cycle_len = std::max(1, c->thermo.cycle_len);
-    st.target_rate = c->thermo.target_rate;
+    st.ln_target_rate = std::log(c->thermo.target_rate);
     st.period = std::max(1, c->thermo.period);
     st.step0 = c->step;
     st.nsteps = steps;
@@ -1408,6 +1408,21 @@ extern "C" adx_status adx_walkers_export(adx_ctx *c, void *dev_seqs, void *dev_s
         HIP_TRY(hipMemcpyAsync(dev_scores, c->cur_score.p, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
     HIP_TRY(hipStreamSynchronize(c->pb.stream));
     return ADX_OK;
+}
+
+extern "C" adx_status adx_walkers_import_after(adx_ctx *c, const void *dev_seqs, const void *dev_scores,
+                                               void *producer_stream) {
+    if (!c) return fail(ADX_EINVAL, "adx_walkers_import_after: null context");
+    if (producer_stream) {
+        // order the copies after the producer's queued writes (device-side wait, no host sync)
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, hipStream_t(producer_stream));
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->pb.stream, ev, 0);
+        hipEventDestroy(ev);
+        HIP_TRY(e);
+    }
+    return adx_walkers_import(c, dev_seqs, dev_scores);
 }
 
 extern "C" adx_status adx_walkers_import(adx_ctx *c, const void *dev_seqs, const void *dev_scores) {

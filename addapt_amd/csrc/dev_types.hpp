@@ -214,7 +214,7 @@ struct StepArgs {
     int thermo_kind;
     double t_fixed, t_hi, t_lo;
     int cycle_len;
-    double target_rate;
+    double ln_target_rate;   // log(target rate), host libm (the reference divides by log(rate), sampling.cc:395)
     int period;
     long long step0;            // global step index of the first step of this launch
     int nsteps;

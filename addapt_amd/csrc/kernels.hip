@@ -1862,7 +1862,7 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
                 // land exactly where the reference's do
                 const int k = n / 2;
                 nth_element_libstdcxx(tr, k, n);
-                const double t = tr[k] / log(st.target_rate);
+                const double t = tr[k] / st.ln_target_rate;
                 Tn = (t < 0.0) ? 0.0 : t;
                 st.auto_T[w] = Tn;
                 st.ntrain[w] = 0;

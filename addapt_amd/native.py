@@ -75,7 +75,7 @@ EXPORTS = [
     "adx_last_kernel_split_ms",
     "adx_last_kernel_names",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
-    "adx_walkers_import", "adx_set_temperature", "adx_bppm_batch",
+    "adx_walkers_import", "adx_walkers_import_after", "adx_set_temperature", "adx_bppm_batch",
 ]
 
 _lib = None
@@ -112,6 +112,7 @@ def lib():
         L.adx_last_kernel_names.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_char_p, C.c_int]
         L.adx_walkers_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_walkers_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.adx_walkers_import_after.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_set_temperature.argtypes = [C.c_void_p, C.c_double]
         L.adx_walkers_download.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
                                            C.POINTER(C.c_int64)]
@@ -341,8 +342,15 @@ class Engine:
         scores (W float64) into caller-owned device buffers (raw pointers)."""
         _check(lib().adx_walkers_export(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
 
-    def import_walkers(self, dev_seqs_ptr, dev_scores_ptr):
-        _check(lib().adx_walkers_import(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+    def import_walkers(self, dev_seqs_ptr, dev_scores_ptr, after_stream=None):
+        """Copy configurations back in; `after_stream` (a raw HIP stream handle,
+        e.g. torch.cuda.current_stream().cuda_stream) orders the copy after the
+        work queued there without a host synchronisation."""
+        if after_stream is None:
+            _check(lib().adx_walkers_import(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+        else:
+            _check(lib().adx_walkers_import_after(self.ptr, C.c_void_p(dev_seqs_ptr),
+                                                  C.c_void_p(dev_scores_ptr), C.c_void_p(after_stream)))
 
     def set_temperature(self, t):
         _check(lib().adx_set_temperature(self.ptr, float(t)))

@@ -37,6 +37,20 @@ def partner(rank, world, round_idx):
     return p if 0 <= p < world else None
 
 
+def digests(seqs, scores):
+    """64-bit digest per walker slot of its configuration (sequence codes and
+    the score's bit pattern), host numpy in, uint64 [W] out: a swap audit
+    compares these across the ranks of a pair."""
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    sb = np.ascontiguousarray(scores, dtype=np.float64).view(np.uint8).reshape(-1, 8)
+    rows = np.concatenate([seqs, sb], axis=1).astype(np.uint64)
+    h = np.full(rows.shape[0], 0xCBF29CE484222325, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(rows.shape[1]):   # FNV-1a over the row's bytes
+            h = (h ^ rows[:, c]) * np.uint64(0x100000001B3)
+    return h
+
+
 def _key(seed, round_idx, lo_rank):
     """63-bit generator key shared by both ranks of a pair."""
     k = 0x9E3779B97F4A7C15
@@ -76,12 +90,14 @@ def exchange_round(dist, round_idx, rank, world, temps, seqs, scores, seed=0):
     RCCL, CPU for gloo), updated in place.  The pair's configurations travel
     as ONE packed [W, N + 8] byte buffer each way (one send + one receive,
     device to device over RCCL/xGMI); the decision and the swap stay on the
-    device.  Returns (attempted, accepted) as device tensors' values."""
+    device.  Returns (attempted, accepted): attempted a host int (W or 0),
+    accepted a 0-d tensor on the walkers' device (summed by the caller at the
+    end of the run, so a round needs no host read-back)."""
     import torch
 
     p = partner(rank, world, round_idx)
     if p is None:
-        return 0, 0
+        return 0, None
     W, N = seqs.shape
     packed = torch.cat([seqs, scores.view(torch.uint8).reshape(W, 8)], dim=1).contiguous()
     # gloo (CPU tests) moves host tensors only
@@ -104,21 +120,27 @@ def exchange_round(dist, round_idx, rank, world, temps, seqs, scores, seed=0):
                     temps[lo], temps[hi]).to(seqs.device)
     seqs.copy_(torch.where(acc[:, None], other_seqs, seqs))
     scores.copy_(torch.where(acc, other_scores, scores))
-    return int(acc.numel()), int(acc.sum())
+    return int(acc.numel()), acc.sum()
 
 
 def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda", observe=None):
     """Advance `engine` (a native.Engine of this rank, fixed thermostat) by
     `steps` MC steps with an exchange every `interval` steps.  `observe`
-    (tests): called per round with host copies (round, seqs, scores before,
-    seqs, scores after the exchange)."""
+    (tests, audits): called per round with host copies (round, partner, seqs,
+    scores before, seqs, scores after the exchange).
+
+    Per round the host does no read-back of its own: the accept count stays a
+    device tensor (summed once after the last round), and the import is
+    ordered after the exchange's device work by a stream wait
+    (adx_walkers_import_after) instead of a device synchronisation."""
     import torch
 
     engine.set_temperature(temps[rank])
     W, N = engine.W, engine.N
     seqs = torch.empty((W, N), dtype=torch.uint8, device=device)
     scores = torch.empty((W,), dtype=torch.float64, device=device)
-    done, rnd, att, acc = 0, 0, 0, 0
+    done, rnd, att = 0, 0, 0
+    acc = torch.zeros((), dtype=torch.int64, device=device)
     while done < steps:
         k = min(interval, steps - done)
         engine.run_steps(k)
@@ -128,11 +150,12 @@ def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda"
             before = (seqs.cpu().numpy().copy(), scores.cpu().numpy().copy()) if observe else None
             a, b = exchange_round(dist, rnd, rank, world, temps, seqs, scores, seed)
             if observe:
-                observe(rnd, before[0], before[1], seqs.cpu().numpy().copy(), scores.cpu().numpy().copy())
-            if seqs.is_cuda:
-                torch.cuda.synchronize()   # the engine copies on its own stream
-            engine.import_walkers(seqs.data_ptr(), scores.data_ptr())
+                observe(rnd, partner(rank, world, rnd), before[0], before[1],
+                        seqs.cpu().numpy().copy(), scores.cpu().numpy().copy())
+            stream = torch.cuda.current_stream(seqs.device).cuda_stream if seqs.is_cuda else None
+            engine.import_walkers(seqs.data_ptr(), scores.data_ptr(), after_stream=stream)
             att += a
-            acc += b
+            if b is not None:
+                acc += b
             rnd += 1
-    return {"rounds": rnd, "attempted": att, "accepted": acc}
+    return {"rounds": rnd, "attempted": att, "accepted": int(acc)}

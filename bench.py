@@ -63,6 +63,10 @@ def parse():
     ap.add_argument("--replica-interval", type=int, default=0,
                     help="BASELINE config 5: one temperature rung per rank (0.5*1.5^r), RCCL swap of "
                          "walker configurations between neighbouring rungs every K steps (N > 1 only)")
+    ap.add_argument("--replica-audit", default=None, metavar="DIR",
+                    help="replica exchange: each rank writes DIR/rank<r>.npz with per-round configuration "
+                         "digests before/after the swap and sampled final walkers (tests; off the timed path "
+                         "only in the sense that it adds host copies per round)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic "
                          "(default profiles/traffic_latest_<fold>.json)")
@@ -237,8 +241,21 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     barrier()
     t0 = time.perf_counter()
     rx = None
+    audit = None
     if replica_mode:
-        rx = replica.run(eng, dist, rank, world, steps, a.replica_interval, temps, seed=0, device="cuda")
+        observe = None
+        if a.replica_audit:
+            audit = {"round": [], "partner": [], "before": [], "after": [], "moved": []}
+
+            def observe(rnd, p, s0, c0, s1, c1):
+                audit["round"].append(rnd)
+                audit["partner"].append(-1 if p is None else p)
+                d0, d1 = replica.digests(s0, c0), replica.digests(s1, c1)
+                audit["before"].append(d0)
+                audit["after"].append(d1)
+                audit["moved"].append(int((d0 != d1).sum()))
+        rx = replica.run(eng, dist, rank, world, steps, a.replica_interval, temps, seed=0, device="cuda",
+                         observe=observe)
     else:
         eng.run_steps(steps)
     barrier()
@@ -247,8 +264,22 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     score_ms, launches = eng.last_score_kernel_ms()   # the step's score window, per launch
     inside_ms, outside_ms = eng.last_kernel_split_ms()   # the same window split per kernel
     inside_name, outside_name = eng.last_kernel_names()  # what the engine launched
-    _, _, c1 = eng.download()
+    fin_seqs, fin_scores, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device=dev)
+    if audit is not None:
+        import numpy as np
+
+        os.makedirs(a.replica_audit, exist_ok=True)
+        pick = sorted(set(range(0, W, max(1, W // 8))) | {W - 1})
+        np.savez(os.path.join(a.replica_audit, "rank%d.npz" % rank),
+                 round=np.array(audit["round"]), partner=np.array(audit["partner"]),
+                 before=np.array(audit["before"], dtype=np.uint64),
+                 after=np.array(audit["after"], dtype=np.uint64), moved=np.array(audit["moved"]),
+                 temperature=np.array([temps[rank]]), accepted=np.array([rx["accepted"]]),
+                 attempted=np.array([rx["attempted"]]), sample_slots=np.array(pick),
+                 sample_seqs=np.array([fin_seqs[w] for w in pick]),
+                 sample_scores=fin_scores[pick], counters=c1 - c0, template=np.array([tmpl]),
+                 active=np.array([active]), fold=np.array([fold]))
     value = W * steps * world / elapsed
 
     # algorithmic work of the launch: scored steps x the folds' (+ outside passes') terms

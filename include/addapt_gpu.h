@@ -223,6 +223,13 @@ adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_
  * complete (its stream synchronized) before adx_walkers_import. */
 adx_status adx_walkers_export(adx_ctx *ctx, void *dev_seqs, void *dev_scores);
 adx_status adx_walkers_import(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores);
+/* adx_walkers_import ordered after the work already queued on the caller's
+ * HIP stream `producer_stream` (e.g. torch's current stream holding the
+ * exchange's copies): the context's stream waits on an event recorded there,
+ * so the caller needs no host synchronisation before the import.  NULL = the
+ * plain import. */
+adx_status adx_walkers_import_after(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores,
+                                    void *producer_stream);
 /* Temperature of an ADX_THERMO_FIXED context (one rung of a replica ladder). */
 adx_status adx_set_temperature(adx_ctx *ctx, double t);
 

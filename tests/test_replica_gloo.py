@@ -40,7 +40,8 @@ def _worker(rank, world, port, W, N, rounds, q):
         temps = replica.ladder_temperatures(world)
         stats = []
         for r in range(rounds):
-            stats.append(replica.exchange_round(dist, r, rank, world, temps, seqs, scores, seed=7))
+            a, b = replica.exchange_round(dist, r, rank, world, temps, seqs, scores, seed=7)
+            stats.append((a, 0 if b is None else int(b)))
         # numpy copies travel by value (torch tensors go through shared memory that
         # can vanish when this process exits before the parent reads the queue)
         q.put((rank, (start[0].numpy().copy(), start[1].numpy().copy()),
@@ -121,7 +122,7 @@ class _HostEngine:
         ctypes.memmove(seqs_ptr, self.seqs.data_ptr(), self.W * self.N)
         ctypes.memmove(scores_ptr, self.scores.data_ptr(), self.W * 8)
 
-    def import_walkers(self, seqs_ptr, scores_ptr):
+    def import_walkers(self, seqs_ptr, scores_ptr, after_stream=None):
         import ctypes
 
         ctypes.memmove(self.seqs.data_ptr(), seqs_ptr, self.W * self.N)
@@ -136,7 +137,7 @@ def _ladder_worker(rank, world, port, W, N, steps, interval, q):
         temps = replica.ladder_temperatures(world)
         rounds = []
 
-        def observe(rnd, s0, c0, s1, c1):
+        def observe(rnd, _p, s0, c0, s1, c1):
             rounds.append((rnd, int((c0 != c1).sum())))
 
         stats = replica.run(eng, dist, rank, world, steps, interval, temps, seed=11, device="cpu",

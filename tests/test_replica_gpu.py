@@ -115,7 +115,7 @@ def _rung_config5(rank, world, port, q):
         eng.walkers_init(ids, workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + ids[0]))
         rounds = []
 
-        def observe(rnd, s0, sc0, s1, sc1):
+        def observe(rnd, _p, s0, sc0, s1, sc1):
             # per round: which slots changed, and hashes of the configurations
             changed = np.nonzero((s0 != s1).any(axis=1) | (sc0 != sc1))[0]
             # deterministic across processes (Python's hash() is salted per process)
