@@ -25,6 +25,7 @@ size_t lds_bytes(const KArgs &ka, bool qbm, int nt);
 hipError_t launch_score(const KArgs &ka, bool qbm, const uint8_t *seqs, int W, double *scores,
                         double *terms, float *dG, hipStream_t stream);
 hipError_t launch_steps(const KArgs &ka, bool qbm, const StepArgs &st, hipStream_t stream, hipEvent_t *evs);
+hipError_t launch_rescore(const KArgs &ka, const StepArgs &st, double *tv, hipStream_t stream);
 const char *inside_kernel_name(const KArgs &ka);
 size_t pf_ring_lds(const KArgs &ka);
 size_t outside_ring_lds(const KArgs &ka);
@@ -674,8 +675,8 @@ struct Problem {
         return ADX_OK;
     }
 
-    // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
-    adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
+    // the per-walker buffers a fold of W walkers writes (grow-only)
+    adx_status prepare(int W) {
         adx_status so = ensure_ovf(W);
         if (so) return so;
         so = ensure_gstep(W);
@@ -684,11 +685,15 @@ struct Problem {
             const size_t need = pf_ring_scratch_floats(kargs(), W);
             if (dRingScr.n < need) HIP_TRY(dRingScr.alloc(need));
         }
-        if (!pairs.empty()) {
-            adx_status s = ensure_pairs(W);
-            if (s) return s;
+        return pairs.empty() ? ADX_OK : ensure_pairs(W);
+    }
+
+    // Score W sequences (device pointer of W*Nraw codes); outputs are device pointers.
+    adx_status score(const uint8_t *dseqs, int W, double *dscores, double *dterms, float *ddG) {
+        adx_status so = prepare(W);
+        if (so) return so;
+        if (!pairs.empty())
             HIP_TRY(launch_bppm(kargs(), dseqs, W, nullptr, nullptr, 0, dPairP.p, dScratch.p, stream));
-        }
         HIP_TRY(launch_score(kargs(), qbm, dseqs, W, dscores, dterms, ddG, stream));
         return ADX_OK;
     }
@@ -1175,6 +1180,28 @@ static void mt_seed_host(uint32_t seed, uint32_t *mt) {
     mt[624] = 624;
 }
 
+// Every walker's current configuration folded from scratch by the MC step's
+// kernels (kernels.hip launch_rescore): fresh scores to prop_score, term
+// values to dtv (device, optional), fresh tables adopted.
+static adx_status rescore_walkers(adx_ctx *c, double *dtv) {
+    Problem &pb = c->pb;
+    const int W = c->W;
+    adx_status s = pb.prepare(W);
+    if (s) return s;
+    StepArgs st{};
+    st.cur_seq = c->cur_seq.p;
+    st.prop_seq = c->prop_seq.p;
+    st.prop_score = c->prop_score.p;
+    st.changed = c->changed.p;
+    st.Nraw = pb.Nraw;
+    st.W = W;
+    pb.state_on = true;
+    const KArgs ka = pb.kargs();
+    pb.state_on = false;
+    HIP_TRY(launch_rescore(ka, st, dtv, pb.stream));
+    return ADX_OK;
+}
+
 extern "C" adx_status adx_walkers_init(adx_ctx *c, int W, const char *seqs, const uint32_t *seeds) {
     if (!c || W <= 0 || !seeds) return fail(ADX_EINVAL, "adx_walkers_init: bad argument");
     Problem &pb = c->pb;
@@ -1214,15 +1241,29 @@ extern "C" adx_status adx_walkers_init(adx_ctx *c, int W, const char *seqs, cons
     HIP_TRY(hipMemsetAsync(c->err.p, 0, sizeof(int) * W, pb.stream));
     std::vector<double> t0(W, c->thermo.t_init);
     HIP_TRY(hipMemcpyAsync(c->auto_T.p, t0.data(), sizeof(double) * W, hipMemcpyHostToDevice, pb.stream));
-    // initial score (sampling.cc:40); it also stores the walkers' first tables
+    // initial score (sampling.cc:40) with the MC step's own kernels; it also
+    // stores the walkers' first tables
     adx_status s = pb.alloc_state(W);
     if (s) return s;
-    pb.state_on = true;
-    s = pb.score(c->cur_seq.p, W, c->cur_score.p, nullptr, nullptr);
-    pb.state_on = false;
+    s = rescore_walkers(c, nullptr);
     if (s) return s;
-    HIP_TRY(hipMemsetAsync(pb.dCur.p, 0, W, pb.stream));
-    HIP_TRY(hipMemsetAsync(pb.dValid.p, 1, W, pb.stream));
+    HIP_TRY(hipMemcpyAsync(c->cur_score.p, c->prop_score.p, sizeof(double) * W, hipMemcpyDeviceToDevice, pb.stream));
+    HIP_TRY(hipStreamSynchronize(pb.stream));
+    return ADX_OK;
+}
+
+extern "C" adx_status adx_walkers_rescore(adx_ctx *c, double *scores, double *term_values) {
+    if (!c || !scores) return fail(ADX_EINVAL, "adx_walkers_rescore: null argument");
+    if (c->W <= 0) return fail(ADX_ESTATE, "adx_walkers_rescore before adx_walkers_init");
+    Problem &pb = c->pb;
+    const int W = c->W, ntt = pb.n_terms * pb.n_ctx_eff;
+    DevBuf<double> dtv;
+    if (term_values && ntt > 0) HIP_TRY(dtv.alloc(size_t(W) * ntt));
+    adx_status s = rescore_walkers(c, dtv.p);
+    if (s) return s;
+    HIP_TRY(hipMemcpyAsync(scores, c->prop_score.p, sizeof(double) * W, hipMemcpyDeviceToHost, pb.stream));
+    if (dtv.p)
+        HIP_TRY(hipMemcpyAsync(term_values, dtv.p, sizeof(double) * W * ntt, hipMemcpyDeviceToHost, pb.stream));
     HIP_TRY(hipStreamSynchronize(pb.stream));
     return ADX_OK;
 }

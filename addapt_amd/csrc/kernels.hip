@@ -2254,6 +2254,52 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
 }
 
+// The score window of one MC step for the walkers flagged in `changed`: the
+// proposals' folds (prop_seq; incremental against the stored tables where
+// tab_valid allows), the outside pass when terms read base-pair probabilities,
+// the scores (prop_score) and term values (tv, optional).  evs (optional, 4):
+// window start, outside pass start, outside pass end, window end.
+static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *changed, double *tv,
+                                hipStream_t stream, hipEvent_t *evs) {
+    if (evs) (void)hipEventRecord(evs[0], stream);
+    hipError_t e;
+    if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
+        // inside folds first (they write the proposal's tables), then the outside
+        // pass on those tables, then the scores with the pair probabilities
+        KArgs ki = ka;
+        ki.pair_p = nullptr;
+        e = launch_score_m(ki, st.prop_seq, st.W, st.prop_score, nullptr, ka.gstep, changed, stream);
+        if (e != hipSuccess) return e;
+        if (evs) (void)hipEventRecord(evs[1], stream);
+        // lanes = cells outside kernel (outside_cells.hip) where it covers the
+        // length, else bppm_kernel on the same stored tables
+        e = ka.pf_ring ? launch_outside_ring(ka, st.prop_seq, st.W, changed, const_cast<double *>(ka.pair_p),
+                                             stream)
+            : outside_is_cells(ka)
+                ? launch_outside_cells(ka, st.prop_seq, st.W, changed, const_cast<double *>(ka.pair_p),
+                                       choose_p(ka), stream)
+                : launch_bppm_r(ka, st.prop_seq, st.W, changed, nullptr, 0, const_cast<double *>(ka.pair_p),
+                                ka.bppm_scratch, stream, true);
+        if (e != hipSuccess) return e;
+        if (evs) (void)hipEventRecord(evs[2], stream);
+        hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, changed,
+                           st.prop_score, tv);
+        e = hipGetLastError();
+    } else {
+        // events 1 / 2 bracket the outside pass (here before the folds; none: empty)
+        if (evs) (void)hipEventRecord(evs[1], stream);
+        if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
+            e = launch_bppm(ka, st.prop_seq, st.W, changed, nullptr, 0, const_cast<double *>(ka.pair_p),
+                            ka.bppm_scratch, stream);
+            if (e != hipSuccess) return e;
+        }
+        if (evs) (void)hipEventRecord(evs[2], stream);
+        e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, changed, stream);
+    }
+    if (evs) (void)hipEventRecord(evs[3], stream);
+    return e;
+}
+
 // evs (optional): 4 * nsteps events per step: window start, outside pass
 // start, outside pass end, window end (score written); the inside share of a
 // window is the window minus its outside pass (adx_api.cpp)
@@ -2262,48 +2308,46 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
     for (int s = 0; s < st.nsteps; s++) {
         hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
-        // the event window covers the outside pass too when the terms read base-pair
-        // probabilities (bench.py divides bppm + score work by it)
-        if (evs) (void)hipEventRecord(evs[4 * s], stream);
-        hipError_t e;
-        if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
-            // inside folds first (they write the proposal's tables), then the outside
-            // pass on those tables, then the scores with the pair probabilities
-            KArgs ki = ka;
-            ki.pair_p = nullptr;
-            e = launch_score_m(ki, st.prop_seq, st.W, st.prop_score, nullptr, ka.gstep, st.changed, stream);
-            if (e != hipSuccess) return e;
-            if (evs) (void)hipEventRecord(evs[4 * s + 1], stream);
-            // lanes = cells outside kernel (outside_cells.hip) where it covers the
-            // length, else bppm_kernel on the same stored tables
-            e = ka.pf_ring ? launch_outside_ring(ka, st.prop_seq, st.W, st.changed, const_cast<double *>(ka.pair_p),
-                                                 stream)
-                : outside_is_cells(ka)
-                    ? launch_outside_cells(ka, st.prop_seq, st.W, st.changed, const_cast<double *>(ka.pair_p),
-                                           choose_p(ka), stream)
-                    : launch_bppm_r(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
-                                    ka.bppm_scratch, stream, true);
-            if (e != hipSuccess) return e;
-            if (evs) (void)hipEventRecord(evs[4 * s + 2], stream);
-            hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, st.changed,
-                               st.prop_score, tv);
-            e = hipGetLastError();
-        } else {
-            // events 1 / 2 bracket the outside pass (here before the folds; none: empty)
-            if (evs) (void)hipEventRecord(evs[4 * s + 1], stream);
-            if (ka.n_pairs > 0) {   // base-pair probabilities the score terms read (outside pass)
-                e = launch_bppm(ka, st.prop_seq, st.W, st.changed, nullptr, 0, const_cast<double *>(ka.pair_p),
-                                ka.bppm_scratch, stream);
-                if (e != hipSuccess) return e;
-            }
-            if (evs) (void)hipEventRecord(evs[4 * s + 2], stream);
-            e = launch_score_m(ka, st.prop_seq, st.W, st.prop_score, tv, nullptr, st.changed, stream);
-        }
-        if (evs) (void)hipEventRecord(evs[4 * s + 3], stream);
+        hipError_t e = launch_window(ka, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,
                            ka.tab ? ka.cur_slot : nullptr);
     }
+    return hipGetLastError();
+}
+
+__global__ void rescore_begin_kernel(int W, int *changed, uint8_t *tab_valid) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    changed[w] = 1;
+    if (tab_valid) tab_valid[w] = 0;
+}
+
+__global__ void rescore_end_kernel(int W, uint8_t *cur_slot, uint8_t *tab_valid, const int *ovf) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    // the fresh tables of the (unchanged) current sequence are in the other slot;
+    // an MFE fold that left the 16-bit range (re-folded in FP32) wrote none
+    cur_slot[w] = uint8_t(1 - cur_slot[w]);
+    tab_valid[w] = (ovf && ovf[w]) ? 0 : 1;
+}
+
+// Every walker's current configuration folded and scored FROM SCRATCH with the
+// MC step's own kernels (launch_window: the same inside, outside and combine
+// launches, tables written to the walker's other slot and then adopted): the
+// walkers' first scores (adx_walkers_init) and adx_walkers_rescore, so stored
+// scores, incremental refolds and a fresh fold agree bit for bit.  Scores land
+// in st.prop_score (tv: term values, optional); no move, no Metropolis.
+hipError_t launch_rescore(const KArgs &ka, const StepArgs &st, double *tv, hipStream_t stream) {
+    hipError_t e = hipMemcpyAsync(st.prop_seq, st.cur_seq, size_t(st.W) * st.Nraw, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return e;
+    const dim3 g((st.W + 255) / 256), b(256);
+    hipLaunchKernelGGL(rescore_begin_kernel, g, b, 0, stream, st.W, st.changed, ka.tab ? ka.tab_valid : nullptr);
+    e = launch_window(ka, st, st.changed, tv, stream, nullptr);
+    if (e != hipSuccess) return e;
+    if (ka.tab)
+        hipLaunchKernelGGL(rescore_end_kernel, g, b, 0, stream, st.W, ka.cur_slot, ka.tab_valid,
+                           ka.mode == 1 ? ka.ovf : nullptr);
     return hipGetLastError();
 }
 

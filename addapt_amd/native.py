@@ -76,6 +76,7 @@ EXPORTS = [
     "adx_last_kernel_names",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
     "adx_walkers_import", "adx_walkers_import_after", "adx_set_temperature", "adx_bppm_batch",
+    "adx_walkers_rescore",
 ]
 
 _lib = None
@@ -118,6 +119,7 @@ def lib():
                                            C.POINTER(C.c_int64)]
         L.adx_score_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double), C.POINTER(C.c_float)]
+        L.adx_walkers_rescore.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.adx_bppm_batch.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.c_int,
                                      C.POINTER(C.c_double)]
         L.adx_variant_desc.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int),
@@ -372,6 +374,17 @@ class Engine:
         a, b = C.create_string_buffer(256), C.create_string_buffer(256)
         _check(lib().adx_last_kernel_names(self.ptr, a, 256, b, 256))
         return a.value.decode(), b.value.decode()
+
+    def rescore(self):
+        """(scores, term values) of every walker's current configuration folded
+        from scratch by the MC step's own kernels (adx_walkers_rescore); the
+        stored scores are not touched."""
+        W = self.W
+        sc = np.zeros(W, np.float64)
+        tv = np.zeros(W * max(1, self.n_terms_total), np.float64)
+        _check(lib().adx_walkers_rescore(self.ptr, sc.ctypes.data_as(C.POINTER(C.c_double)),
+                                         tv.ctypes.data_as(C.POINTER(C.c_double))))
+        return sc, tv.reshape(W, -1)[:, :self.n_terms_total]
 
     def download(self):
         W = self.W

@@ -214,6 +214,15 @@ adx_status adx_last_kernel_names(const adx_ctx *ctx, char *inside, int inside_le
 
 adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_t *counters);
 
+/* Fold and score every walker's CURRENT configuration from scratch with the
+ * MC step's own kernels (the same inside, outside and combine launches as
+ * adx_run_steps, no stored tables read), adopt the fresh tables and write the
+ * fresh scores[W] (and term_values[W*n_terms*max(1,n_contexts)], optional).
+ * The stored scores are left alone: a caller compares the two to check that
+ * incremental refolds equal scratch folds bit for bit.  adx_walkers_init
+ * computes the walkers' first scores this way (sampling.cc:40). */
+adx_status adx_walkers_rescore(adx_ctx *ctx, double *scores, double *term_values);
+
 /* Replica exchange (BASELINE config 5): copy the walkers' configurations --
  * sequence codes (W*N bytes, 1..4 = A,C,G,U) and scores (W doubles) -- to or
  * from caller-owned DEVICE buffers on the context's GPU (e.g. torch tensors

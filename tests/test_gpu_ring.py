@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from addapt_amd import workloads
+from parity_bounds import close_score, close_term, score_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -85,7 +86,7 @@ def test_ring_score_batch(native, oracle, N):
     sf = oracle.ScoreFunction(terms, aptamer=m)
     for w in range(12):
         ref, tref = sf.score(seqs[w], [active])
-        assert abs(sc[w] - ref) <= 2e-3, (w, sc[w], ref)
+        assert close_score(sc[w], ref, tref, terms), (w, sc[w], ref, score_bound(tref, terms))
 
 
 def _replay(native, oracle, N, seeds, steps, contexts=None, macro_extra=None):
@@ -111,9 +112,10 @@ def _replay(native, oracle, N, seeds, steps, contexts=None, macro_extra=None):
         for s in range(steps):
             if ref["outcome"][s] != 2:
                 a, b = tr["proposed_score"][s, w], ref["proposed_score"][s]
-                assert abs(a - b) <= 2e-3, (N, w, s, a, b)
+                assert close_score(a, b, tr["term_values"][s, w], terms), (N, w, s, a, b)
         assert final[w].upper() == ref["seq"].upper(), w
-        assert abs(scores[w] - ref["score"]) <= 2e-3
+        fref, ftv = sf.score(ref["seq"], macro)
+        assert close_score(scores[w], ref["score"], ftv, terms), (N, w, scores[w], ref["score"])
         assert list(counters[w]) == ref["counters"]
 
 

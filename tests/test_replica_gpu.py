@@ -13,6 +13,14 @@ import torch.multiprocessing as mp
 from addapt_amd import workloads
 
 
+def _rel_err(sf, score, seq, active):
+    """|stored - oracle| over the derived score bound (tests/parity_bounds.py)."""
+    from parity_bounds import score_bound
+
+    ref, tv = sf.score(seq, [active])
+    return abs(score - ref) / score_bound(tv, workloads.default_objective())
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -69,7 +77,7 @@ def _rung(rank, world, port, q):
         seqs, scores, counters = eng.download()
         motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
         sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
-        err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in range(W))
+        err = max(_rel_err(sf, scores[w], seqs[w], active) for w in range(W))
         q.put((rank, stats, float(err), int(counters.sum())))
     finally:
         dist.destroy_process_group()
@@ -89,7 +97,7 @@ def test_two_rung_ladder():
         assert p.exitcode == 0
     for rank, stats, err, n in res:
         assert stats["rounds"] == 4
-        assert err <= 2e-3          # imported scores still describe the imported sequences
+        assert err <= 1.0           # imported scores still describe the imported sequences
         assert n == 16 * 20
     assert res[0][1]["attempted"] > 0
 
@@ -128,7 +136,7 @@ def _rung_config5(rank, world, port, q):
         motif = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus())
         sf = O.ScoreFunction(workloads.default_objective(), aptamer=motif)
         sample = list(range(0, W, W // 8))
-        err = max(abs(scores[w] - sf.score(seqs[w], [active])[0]) for w in sample)
+        err = max(_rel_err(sf, scores[w], seqs[w], active) for w in sample)
         q.put((rank, stats, rounds, float(err), counters.sum(axis=0).tolist()))
     finally:
         dist.destroy_process_group()
@@ -167,5 +175,5 @@ def test_config5_ladder_at_workload():
     assert exchanged > 0
     assert r0[1]["accepted"] == r1[1]["accepted"]   # both ranks took the same decisions
     for rank in (0, 1):
-        assert res[rank][3] <= 2e-3, res[rank][3]
+        assert res[rank][3] <= 1.0, res[rank][3]
         assert sum(res[rank][4]) == W * 15
