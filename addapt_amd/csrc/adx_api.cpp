@@ -1460,7 +1460,7 @@ extern "C" adx_status adx_walkers_import_after(adx_ctx *c, const void *dev_seqs,
         HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         hipError_t e = hipEventRecord(ev, hipStream_t(producer_stream));
         if (e == hipSuccess) e = hipStreamWaitEvent(c->pb.stream, ev, 0);
-        hipEventDestroy(ev);
+        (void)hipEventDestroy(ev);
         HIP_TRY(e);
     }
     return adx_walkers_import(c, dev_seqs, dev_scores);

@@ -1978,10 +1978,10 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
 #ifndef ADX_NT2
 #define ADX_NT2 768     // 12 waves x 168 VGPRs (16 x 128 spills)
 #endif
-#ifndef ADX_NT16
-#define ADX_NT16 512    // packed 16-bit MFE
 #define ADX_STR_(x) #x
 #define ADX_STR(x) ADX_STR_(x)
+#ifndef ADX_NT16
+#define ADX_NT16 512    // packed 16-bit MFE
 #endif
 template <int P, int NT = (P == 2 ? ADX_NT2 : 512)>
 static size_t lds_size(const KArgs &ka, int pl, bool rt) {

@@ -99,6 +99,67 @@ def pf_terms(seq, cst=None):
     return n_int, n_ml
 
 
+def cell_terms(seq, cst=None):
+    """Per-cell term counts of one inside pass, (N+2) x (N+2), 1-based:
+    interior terms of the pairable (i, j) (as pf_terms), its multiloop-closing
+    terms, and the qm split terms of (i, j).  Sums over all cells equal
+    pf_terms; sums over the refolded band give an incremental refold's work."""
+    N = len(seq)
+    S = np.zeros(N + 2, dtype=np.int64)
+    S[1:N + 1] = [CODE.get(c.upper(), 0) for c in seq]
+    ok, up, dn = _hc(cst, N)
+    I = np.arange(N + 2)[:, None]
+    J = np.arange(N + 2)[None, :]
+    pairable = (PAIR[S[:, None], S[None, :]] > 0) & ok & (J - I >= 4)
+    pairable[0, :] = pairable[:, 0] = False
+    pairable[N + 1, :] = pairable[:, N + 1] = False
+    pad = np.zeros((N + 2 + 32, N + 2 + 32), dtype=bool)
+    pad[:N + 2, :N + 2] = pairable
+    upi = up[np.minimum(np.arange(N + 2) + 1, N + 1)][:, None]   # up[i + 1]
+    dnj = dn[np.maximum(np.arange(N + 2) - 1, 0)][None, :]       # dn[j - 1]
+    n_int = np.zeros((N + 2, N + 2), dtype=np.int64)
+    Ii = np.broadcast_to(I, (N + 2, N + 2))
+    Jj = np.broadcast_to(J, (N + 2, N + 2))
+    for n1 in range(0, 31):
+        for n2 in range(0, 31 - n1):
+            P = Ii + 1 + n1
+            Q = Jj - 1 - n2
+            m = pairable & (Q - P >= 4)
+            if n1 > 0:
+                m &= upi >= n1
+            if n2 > 0:
+                m &= dnj >= n2
+            m &= pad[P, np.maximum(Q, 0)]
+            n_int += m
+    n_mlc = np.where(pairable, np.clip(J - I - 10, 0, None), 0)
+    d = J - I
+    n_split = np.where((d >= 4) & (d <= N - 6) & (I >= 1) & (J <= N), d - 3, 0)
+    return n_int, n_mlc, n_split
+
+
+def band_mask(N, m_lo, m_hi, widen=1):
+    """Cells (i, i+d) an incremental refold recomputes for changed positions
+    m_lo..m_hi (1-based): rows max(1, m_lo-w-d) .. min(N-d, m_hi+w), w = widen
+    (1 for the fold cells, 2 for the qm rows; mfe_cells.hip clo/chi, qlo/qhi).
+    m_lo = None: the whole triangle (a fold from scratch)."""
+    I = np.arange(N + 2)[:, None]
+    J = np.arange(N + 2)[None, :]
+    d = J - I
+    tri = (I >= 1) & (J <= N) & (d >= 0)
+    if m_lo is None:
+        return tri
+    return tri & (I >= np.maximum(1, m_lo - widen - d)) & (I <= np.minimum(N - d, m_hi + widen))
+
+
+def band_terms(counts, m_lo, m_hi):
+    """(interior, multiloop) terms of the cells a refold over m_lo..m_hi recomputes."""
+    n_int, n_mlc, n_split = counts
+    N = n_int.shape[0] - 2
+    f = band_mask(N, m_lo, m_hi, 1)
+    q = band_mask(N, m_lo, m_hi, 2)
+    return int(n_int[f].sum()), int(n_mlc[f].sum() + n_split[q].sum())
+
+
 def pf_flops(seq, cst=None):
     a, b = pf_terms(seq, cst)
     return 3 * a + 2 * b

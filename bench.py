@@ -189,7 +189,7 @@ def dry_run(a, rank, world):
         dist.destroy_process_group()
 
 
-def _traffic(a_traffic_json, fold, bppm, length, outside_name):
+def _traffic(a_traffic_json, fold, bppm, length, kernel_name):
     """PMC bytes per launch of the dominant kernel from the summary of this exact
     workload (tools/pmc_traffic.py), or (None, None)."""
     path = a_traffic_json or os.path.join(ROOT, "profiles", "traffic_latest_%s%s%s.json" % (
@@ -199,11 +199,64 @@ def _traffic(a_traffic_json, fold, bppm, length, outside_name):
     with open(path) as f:
         tj = json.load(f)
     traffic = tj.get("bytes_per_launch")
-    if bppm:   # the outside pass's own bytes (the summary holds every kernel of the window)
-        key = outside_name.split("<")[0].split(" ")[0]
+    if bppm:   # that kernel's own bytes (the summary holds every kernel of the window)
+        key = kernel_name.split("<")[0].split(" ")[0]
         own = [k["bytes"] for name, k in tj.get("kernels", {}).items() if key and key in name]
         traffic = own[0] if own else None
     return traffic, os.path.relpath(path, ROOT)
+
+
+def executed_inside_work(eng, cur_seqs, tmpl, active, fold, sample=32):
+    """Work the incremental inside refolds actually execute per scored step.
+
+    One traced step after the timed region (its state is not reused): for up
+    to `sample` scored proposals, the proposal's sequence is the walker's
+    current one with the move applied, the refolded band is the hull of the
+    positions whose base changed (kernels.hip propose_kernel -> chg), and the
+    band's terms are counted per cell (roofline.cell_terms / band_terms) for
+    the 4 folds (apo / holo x unconstrained / active).  Returns (mean executed
+    work per scored step, mean full-fold work of the same proposals, proposals
+    sampled)."""
+    from addapt_amd import roofline
+
+    tr = eng.run_steps(1, trace=True)
+    W = len(cur_seqs)
+    partner = {}
+    stk = []
+    for i, c in enumerate(active):
+        if c == "(":
+            stk.append(i)
+        elif c == ")":
+            a = stk.pop()
+            partner[a], partner[i] = i, a
+    comp = {"A": "U", "U": "A", "G": "C", "C": "G"}
+    ex_sum = full_sum = 0.0
+    n = 0
+    mul = 3 if fold == "pf" else 2
+    for w in range(W):
+        if n >= sample:
+            break
+        if int(tr["outcome"][0, w]) == 2:   # ACCEPT_UNCHANGED: not scored
+            continue
+        cur = cur_seqs[w].upper()
+        p, b = int(tr["position"][0, w]), tr["base"][w]
+        prop = list(cur)
+        prop[p] = b
+        if p in partner:
+            prop[partner[p]] = comp[b]
+        changed = [k for k in range(len(cur)) if prop[k] != cur[k]]
+        if not changed:
+            continue
+        lo, hi = min(changed) + 1, max(changed) + 1
+        ps = "".join(prop)
+        for cst in (None, active):
+            cnt = roofline.cell_terms(ps, cst)
+            ei, em = roofline.band_terms(cnt, lo, hi)
+            fi, fm = roofline.band_terms(cnt, None, None)
+            ex_sum += 2 * (mul * ei + 2 * em)     # apo and holo share the cell work
+            full_sum += 2 * (mul * fi + 2 * fm)
+        n += 1
+    return (ex_sum / n if n else None), (full_sum / n if n else None), n
 
 
 def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, dev, local_rank,
@@ -266,6 +319,10 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     inside_name, outside_name = eng.last_kernel_names()  # what the engine launched
     fin_seqs, fin_scores, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device=dev)
+    # executed (incremental) vs algorithmic inside work, from one traced step
+    # after the timed region (rank 0 reports it)
+    ex_inside, full_inside, ex_n = executed_inside_work(eng, fin_seqs, tmpl, active, fold) \
+        if rank == 0 and not replica_mode else (None, None, 0)
     if audit is not None:
         import numpy as np
 
@@ -298,16 +355,34 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         flop_per_scored += f_out
     scored_pl = scored / max(1, steps)                             # scored walkers per launch
     launch_flops = scored_pl * flop_per_scored                     # per score window (one per step)
-    # the dominant kernel's own time: the outside pass with pair terms, else the
-    # window (inside folds + the score combine)
-    kern_ms, kern_flops = (outside_ms, scored_pl * f_out) if bppm else (score_ms, launch_flops)
+    # the dominant kernel by measured time: with pair terms the longer of the
+    # inside folds and the outside pass, else the window (inside folds + the
+    # score combine)
+    outside_dominant = bppm and outside_ms >= inside_ms
+    if not bppm:
+        kern_ms, kern_flops, kern_name = score_ms, launch_flops, inside_name
+    elif outside_dominant:
+        kern_ms, kern_flops, kern_name = outside_ms, scored_pl * f_out, outside_name
+    else:
+        kern_ms, kern_flops, kern_name = inside_ms, scored_pl * flop_inside, inside_name
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else None
+    # executed work: the inside refolds recompute only the band of cells that
+    # contain a changed position; the outside pass is a full pass.  Scaled from
+    # the sampled proposals' executed / full ratio onto this run's algorithmic count.
+    ex_ratio = (ex_inside / full_inside) if ex_inside and full_inside else None
+    if ex_ratio is None:
+        exec_flops = None
+    elif outside_dominant:
+        exec_flops = kern_flops
+    else:
+        exec_flops = scored_pl * flop_inside * ex_ratio
+    exec_achieved = exec_flops / (kern_ms * 1e-3) / 1e12 if exec_flops and kern_ms > 0 else None
     # incremental-fold state written per scored walker (kernels.hip Inc): 2 fold
     # groups x value arrays (MFE: one packed apo/holo array; PF: two) x
     # (3 cell tables + q5) x 4 B
     cells = (length - 4) * (length - 3) // 2
     state_bytes = 2 * (1 if fold == "mfe" else 2) * (3 * cells + length + 2) * 4
-    traffic, traffic_src = _traffic(traffic_json, fold, bppm, length, outside_name)
+    traffic, traffic_src = _traffic(traffic_json, fold, bppm, length, kern_name)
     peak, peak_note = roofline.valu_peak(fold)
     roof = {
         "bound": "valu",
@@ -317,8 +392,17 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         "frac": (achieved / peak) if achieved else None,
         "traffic": traffic,
         "compute_unit": peak_note,
-        "kernel": (outside_name + " (events around its launch; the window also holds " + inside_name + ")")
-                  if bppm else inside_name,
+        "kernel": (kern_name + " (events around its launch; the window also holds " +
+                   (inside_name if outside_dominant else outside_name) + ")") if bppm else inside_name,
+        "executed_flop_per_launch": exec_flops,
+        "executed_achieved": exec_achieved,
+        "executed_frac": (exec_achieved / peak) if exec_achieved else None,
+        "executed_note": ("inside refolds recompute the cells containing a changed position: "
+                          "%.3f of the full folds' terms over %d sampled proposals (one traced step "
+                          "after the timed region, roofline.band_terms)%s"
+                          % (ex_ratio, ex_n, "; the priced kernel is the full outside pass"
+                             if outside_dominant else "")) if ex_ratio else None,
+        "inside_executed_ratio": ex_ratio,
         "inside_kernel": inside_name,
         "outside_kernel": outside_name or None,
         "traffic_source": traffic_src,
@@ -328,6 +412,8 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         "outside_ms_per_launch": outside_ms if bppm else None,
         "inside_frac": ((scored_pl * flop_inside / (inside_ms * 1e-3) / 1e12) / peak
                         if bppm and inside_ms > 0 else None),
+        "outside_frac": ((scored_pl * f_out / (outside_ms * 1e-3) / 1e12) / peak
+                         if bppm and outside_ms > 0 else None),
         "launches": launches,
         "all_kernels_ms_per_step": kernel_ms / steps,
         "flop_per_scored_step": flop_per_scored,

@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 from addapt_amd import workloads
+from parity_bounds import close_score, close_term, score_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -145,7 +146,7 @@ def test_mc_trajectory_with_pair_terms(native, oracle):
 
 
 @pytest.mark.parametrize("N,motif_pairs", [(60, False), (80, True), (100, False), (110, False), (150, False),
-                                           (150, True)])
+                                           (150, True), ("longest", False)])
 def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
     """Configs 3 / 4 shape: inside folds first (N <= 100: pf_cells_kernel,
     else pf_ring_kernel), the outside pass on the proposal's stored inside tables
@@ -153,7 +154,15 @@ def test_mc_pair_terms_proposed_scores(native, oracle, N, motif_pairs):
     kernel's diagonal-major slot), then the scores.  Every
     scored proposal's score matches the oracle's from-scratch score of that
     proposal (within the derived bound).  motif_pairs: pair terms inside the
-    ligand motif (credited from the motif's closing cell in the holo fold)."""
+    ligand motif (credited from the motif's closing cell in the holo fold).
+    "longest": the longest template a pair-term context accepts (<= 190)."""
+    if N == "longest":
+        for N in range(190, 149, -1):
+            try:
+                _engine(native, workloads.synthetic(N)[0], [workloads.synthetic(N)[1]], _objective(N))
+                break
+            except native.AdxError as e:
+                assert e.status == native.EUNSUPPORTED, e
     tmpl, active = workloads.synthetic(N)
     terms = _objective(N)
     if motif_pairs:

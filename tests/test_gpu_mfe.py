@@ -111,6 +111,30 @@ def test_fold_mfe_motif(native, oracle):
             assert _same(g, oracle.mfe_energy(seq, cst, m)), (seq, g)
 
 
+@pytest.mark.parametrize("mode", ["replace", "auto", "add"])
+def test_engine_holo_mfe_motif_modes(native, oracle, mode):
+    """The engine's MFE holo fold of the THEO aptamer under each motif mode
+    (adx_run_desc.motif_mode): REPLACE and AUTO give RNAfold's printed holo
+    MFE -9.22 kcal/mol with the -9.22 bonus (test_scoring.cc:154), ADD (the
+    default) adds the motif's own loop energies (-10.92); every mode equals
+    the oracle's fold under the same mode."""
+    apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
+    mm = {"add": native.MOTIF_ADD, "replace": native.MOTIF_REPLACE, "auto": native.MOTIF_AUTO}[mode]
+    om = {"add": 0, "replace": 1, "auto": 2}[mode]
+    terms = [("apo", 0, False, 1.0), ("holo", 0, True, 1.0)]
+    eng = native.Engine(apt, ["." * len(apt)], terms, aptamer=(apt, fold, -9.22), motif_mode=mm,
+                        fold_mode="mfe", thermostat=native.make_thermostat("fixed", t=1.0))
+    _, _, dg = eng.score_batch([apt])
+    holo = [v for v in range(eng.info.n_variants) if eng.variant(v)[1] == 1 and eng.variant(v)[2] < 0]
+    assert holo
+    g = float(dg[0, holo[0]])
+    assert _same(g, oracle.mfe_energy(apt, None, oracle.make_motif(apt, fold, -9.22, mode=om))), (mode, g)
+    if mode == "add":
+        assert abs(g - -10.92) <= 0.005, g
+    else:
+        assert abs(g - -9.22) <= 0.005, g
+
+
 def _engine(native, tmpl, macro, terms, thermostat=None, contexts=None):
     apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
     return native.Engine(tmpl, macro, terms, aptamer=apt, contexts=contexts, fold_mode="mfe",

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from addapt_amd import workloads
+from parity_bounds import close_score, close_term, score_bound
 
 pytestmark = pytest.mark.gpu
 

@@ -133,6 +133,45 @@ def test_ring_trajectory_contexts(native, oracle):
     _replay(native, oracle, N, [41, 42, 43], 20, contexts=ctx, macro_extra=other)
 
 
+def test_ring_trajectory_short_variants(native, oracle):
+    """A context mix whose folded lengths straddle the ring threshold (96 and
+    102 nt): the context takes the ring kernel for every variant, including
+    the ones shorter than 101 nt (pf_ring_lds is chosen once per context)."""
+    _replay(native, oracle, 96, [51, 52, 53], 20, contexts=[("", ""), ("AAAAAA", "")])
+
+
+def _longest_context(native):
+    """The longest synthetic template a context accepts (the ring kernels take
+    up to RG_NMAX = 190 nt; the context also sizes the stateless score
+    kernel's LDS layout, adx_api.cpp choose_layout, which ends lower)."""
+    terms = workloads.default_objective()
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    for N in range(190, 149, -1):
+        tmpl, active = workloads.synthetic(N)
+        try:
+            return N, native.Engine(tmpl, [active], terms, aptamer=apt)
+        except native.AdxError as e:
+            assert e.status == native.EUNSUPPORTED, e
+    raise AssertionError("no context above 150 nt")
+
+
+def test_ring_long_score_and_trajectory(native, oracle):
+    """At the longest length a context accepts (>= 150): ensemble energies of
+    every variant vs the FP64 oracle, then a short trajectory replay."""
+    N, eng = _longest_context(native)
+    tmpl, active = workloads.synthetic(N)
+    terms = workloads.default_objective()
+    seqs = workloads.walker_sequences(tmpl, [active], 4)
+    sc, tv, dg = eng.score_batch(seqs)
+    m = _motif(oracle)
+    for v in range(eng.info.n_variants):
+        _, cond, mac = eng.variant(v)
+        for w in range(0, 4, 2):
+            ref = oracle.pf_energy(seqs[w], active if mac >= 0 else None, m if cond == 1 else None)
+            assert abs(dg[w, v] - np.float32(ref)) <= DG_TOL, (N, v, w, dg[w, v], ref)
+    _replay(native, oracle, N, [61, 62], 12)
+
+
 def test_ring_incremental_consistency(native):
     """512 walkers x 40 steps at N = 150: every stored score equals a
     from-scratch score of the final sequence bit for bit."""
@@ -151,3 +190,5 @@ def test_ring_incremental_consistency(native):
     sc, _, _ = eng.score_batch(final)
     bad = np.nonzero(scores != sc)[0]
     assert bad.size == 0, [(int(w), scores[w], sc[w]) for w in bad[:8]]
+    fresh, _ = eng.rescore()   # the step's own kernels from scratch
+    assert (fresh == scores).all()
