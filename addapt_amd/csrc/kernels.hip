@@ -1937,7 +1937,13 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
     }
 }
 
-__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot, uint8_t *cur_slot) {
+// cur_slot / tab_valid (null without stored tables): an accepted proposal's
+// tables become current, and complete (every kernel writes the whole slot),
+// so a walker whose current tables were invalid (imported configuration,
+// MFE fold outside the 16-bit range) refolds incrementally again -- unless
+// this very fold left the 16-bit range (ovf, MFE: its slot is not exact)
+__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot, uint8_t *cur_slot,
+                                                     uint8_t *tab_valid, const int *ovf) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= st.W || st.err[w]) return;
     const bool changed = st.changed[w] == 1;
@@ -1952,7 +1958,10 @@ __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_
         } else {
             outcome = (diff > 0) ? 3 : 1;
             st.cur_score[w] = prop;
-            if (cur_slot) cur_slot[w] ^= 1;   // the proposal's tables become current
+            if (cur_slot) {
+                cur_slot[w] ^= 1;   // the proposal's tables become current
+                tab_valid[w] = (ovf && ovf[w]) ? 0 : 1;
+            }
             const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
             uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
             for (int k = 0; k < st.Nraw; k++) c[k] = p[k];
@@ -2311,7 +2320,8 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         hipError_t e = launch_window(ka, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,
-                           ka.tab ? ka.cur_slot : nullptr);
+                           ka.tab ? ka.cur_slot : nullptr, ka.tab ? ka.tab_valid : nullptr,
+                           ka.mode == 1 ? ka.ovf : nullptr);
     }
     return hipGetLastError();
 }

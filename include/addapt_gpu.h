@@ -229,7 +229,9 @@ adx_status adx_walkers_rescore(adx_ctx *ctx, double *scores, double *term_values
  * swapped between ranks over RCCL).  RNG streams, counters and thermostat
  * state stay with the walker slot: a swap moves configurations between
  * temperatures.  Synchronous; the caller's own writes to the buffers must be
- * complete (its stream synchronized) before adx_walkers_import. */
+ * complete (its stream synchronized) before adx_walkers_import.  An imported
+ * walker folds from scratch until one of its proposals is accepted; from then
+ * on it refolds incrementally on that proposal's tables. */
 adx_status adx_walkers_export(adx_ctx *ctx, void *dev_seqs, void *dev_scores);
 adx_status adx_walkers_import(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores);
 /* adx_walkers_import ordered after the work already queued on the caller's

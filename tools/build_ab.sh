@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B builds of the engine into addapt_amd/_lib/ablate/lib_<name>.so: each spec
-# name=<git rev or "tree">:<kernel file>:<flags> replaces ONE kernel source by its
-# version at that revision (the rest is the working tree) and adds the flags
+# name=<git rev or "tree">:<kernel files, comma-separated>:<flags> replaces those
+# kernel sources by their version at that revision (the rest is the working
+# tree; host code and headers always from the tree) and adds the flags
 # ("__" for spaces).  Select one with ADX_LIB=addapt_amd/_lib/ablate/lib_<name>.so
 # (tools/gpu_run.sh "libs" step).
 #   tools/build_ab.sh new=tree:mfe_cells.hip: old=HEAD:mfe_cells.hip: stamp=tree:mfe_cells.hip:-DADX_STAMP
@@ -24,12 +25,15 @@ for spec in "$@"; do
   flags=${flags//__/ }
   mkdir -p $T/$name
   cp $SRC/* $T/$name/
-  [ "$rev" != "tree" ] && git -C $ROOT show $rev:addapt_amd/csrc/$file > $T/$name/$file
+  files=${file//,/ }
+  if [ "$rev" != "tree" ]; then
+    for f in $files; do git -C $ROOT show $rev:addapt_amd/csrc/$f > $T/$name/$f; done
+  fi
   (
-  $H $flags -c $T/$name/$file -o $OUT/${name}_${file%.hip}.o
+  for f in $files; do $H $flags -c $T/$name/$f -o $OUT/${name}_${f%.hip}.o; done
   objs=""
   for f in kernels mfe_cells outside_cells pf_cells pf_ring outside_ring; do
-    if [ "$f.hip" = "$file" ]; then objs="$objs $OUT/${name}_$f.o"; else objs="$objs $OUT/tree_$f.o"; fi
+    if [[ " $files " == *" $f.hip "* ]]; then objs="$objs $OUT/${name}_$f.o"; else objs="$objs $OUT/tree_$f.o"; fi
   done
   hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_$name.so $objs $OUT/api.o $OUT/energy.o
   ) &

@@ -68,7 +68,7 @@ for step in "$@"; do
       variants=${args%%:*}
       bargs=${args#*:}
       [ "$variants" = "$args" ] && bargs=
-      for k in 1 2; do
+      for k in $(seq ${REPS:-2}); do
         for v in $variants; do
           ADX_LIB=addapt_amd/_lib/ablate/lib_$v.so timeout -k 10 200 python bench.py --no-cpu-baseline \
             --no-sub-records $bargs > $D/${name}_${v}_$k.json 2> $D/${name}_${v}_$k.err
