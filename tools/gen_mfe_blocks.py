@@ -30,7 +30,7 @@ def out_dir():
 
 
 MAXLOOP = 30
-NBLK = 7           # waves 0..6 (wave 7 folds the multiloop qm / mla)
+NBLK = int(os.environ.get("ADX_GEN_NBLK", "7"))   # block waves 0..NBLK-1 (wave 7 folds the multiloop qm / mla)
 SCHED_CHUNK = 1000 # shapes per scheduling window (whole loop sizes)
 KSAT = 5           # nin[k] == nin[KSAT] for k >= KSAT (checked on the host)
 
@@ -83,7 +83,7 @@ def scost(u, S):
 # one-wave roles riding on block waves (mfe_cells.hip), in block-cost units,
 # from the stamps (tools/mfe_mc_stamps.py): finalize lane-set 0 on wave 6, q5
 # on wave 1, the qm1 column minima on wave 3, the list + records on wave 4
-ROLES4 = "6:8,1:7,3:5,4:10"
+ROLES4 = "6:8,1:7,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
 
 
 def role_loads(S):
