@@ -1246,24 +1246,28 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<P> L;
     lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, ka.opt & 3, (ka.opt & 4) != 0, NT / WAVE);
-    const int w = blockIdx.x;
-    if (w >= W) return;
-    if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
-    if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
-    load_ctab(ka, L);
-    for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
-    __syncthreads();
-    const int nt = ka.n_terms * ka.n_ctx_eff;
-    const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
-    bool bad = false;
-    const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, pp, dG ? dG + size_t(w) * ka.n_variants : nullptr,
-                                          terms ? terms + size_t(w) * nt : nullptr, bad, w);
-    if (threadIdx.x == 0) {
-        scores[w] = s;
-        if (SR::NV == 2 && bad && ka.ovf) {
-            ka.ovf[w] = 1;                         // re-folded by the FP32 MinPlus kernel
-            if (ka.tab) ka.tab_valid[w] = 0;       // and folded from scratch next time
+    // walkers blockIdx.x, + gridDim.x, ...: one each with a grid of W; the FP32
+    // refold of the few walkers whose 16-bit fold left the exact range runs on a
+    // short grid that scans the mask (launch_score_m)
+    for (int w = blockIdx.x; w < W; w += gridDim.x) {
+        if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
+        if (mask && mask[w] != 1) continue;  // MC: only walkers whose proposal changed
+        load_ctab(ka, L);
+        for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
+        __syncthreads();
+        const int nt = ka.n_terms * ka.n_ctx_eff;
+        const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
+        bool bad = false;
+        const double s = score_sequence<NT, P, SR>(ka, XS, L.raw, L, pp, dG ? dG + size_t(w) * ka.n_variants : nullptr,
+                                              terms ? terms + size_t(w) * nt : nullptr, bad, w);
+        if (threadIdx.x == 0) {
+            scores[w] = s;
+            if (SR::NV == 2 && bad && ka.ovf) {
+                ka.ovf[w] = 1;                         // re-folded by the FP32 MinPlus kernel
+                if (ka.tab) ka.tab_valid[w] = 0;       // and folded from scratch next time
+            }
         }
+        __syncthreads();   // the LDS tables are the next walker's
     }
 }
 
@@ -1828,7 +1832,7 @@ __device__ void nth_element_libstdcxx(double *a, int k, int n) {
 // One MonteCarlo::apply iteration (sampling.cc:55-99) = three launches on one
 // stream: propose_kernel (thermostat, RNG streams, mutation move, unchanged
 // check; one wave per walker) -> score_kernel masked to the walkers whose
-// sequence changed -> accept_kernel (Metropolis, one thread per walker).
+// sequence changed -> accept_kernel (Metropolis, one wave per walker).
 // Splitting keeps the fold kernel's register allocation free of the MC state.
 __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step, int s) {
     const int w = blockIdx.x;
@@ -1942,29 +1946,35 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
 // so a walker whose current tables were invalid (imported configuration,
 // MFE fold outside the 16-bit range) refolds incrementally again -- unless
 // this very fold left the 16-bit range (ovf, MFE: its slot is not exact)
+// One wave per walker (4 walkers per 256-thread block): every lane takes the
+// (uniform) Metropolis decision, lane 0 writes the walker's state, and an
+// accepted proposal's sequence is copied by the whole wave (coalesced).
 __global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot, uint8_t *cur_slot,
                                                      uint8_t *tab_valid, const int *ovf) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & (WAVE - 1);
     if (w >= st.W || st.err[w]) return;
     const bool changed = st.changed[w] == 1;
     int outcome = 2;  // ACCEPT_UNCHANGED
     const double prop = st.prop_score[w];
+    double diff = 0.0;
     if (changed) {
-        const double diff = prop - st.cur_score[w];
-        st.last_diff[w] = diff;
+        diff = prop - st.cur_score[w];
         const double crit = exp(diff / st.temp[w]);
-        if (crit < st.u[w]) {
-            outcome = 0;
-        } else {
-            outcome = (diff > 0) ? 3 : 1;
-            st.cur_score[w] = prop;
-            if (cur_slot) {
-                cur_slot[w] ^= 1;   // the proposal's tables become current
-                tab_valid[w] = (ovf && ovf[w]) ? 0 : 1;
-            }
-            const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
-            uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
-            for (int k = 0; k < st.Nraw; k++) c[k] = p[k];
+        outcome = (crit < st.u[w]) ? 0 : (diff > 0) ? 3 : 1;
+    }
+    if (outcome == 1 || outcome == 3) {
+        const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
+        uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
+        for (int k = lane; k < st.Nraw; k += WAVE) c[k] = p[k];
+    }
+    if (lane != 0) return;
+    if (changed) st.last_diff[w] = diff;
+    if (outcome == 1 || outcome == 3) {
+        st.cur_score[w] = prop;
+        if (cur_slot) {
+            cur_slot[w] ^= 1;   // the proposal's tables become current
+            tab_valid[w] = (ovf && ovf[w]) ? 0 : 1;
         }
     }
     st.counters[size_t(w) * 4 + outcome] += 1;
@@ -2024,7 +2034,7 @@ size_t lds_bytes(const KArgs &ka, bool /*unused*/, int /*nt*/) {
 
 template <int NT, int P, class SR>
 static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms,
-                                 float *dG, const int *mask, hipStream_t stream) {
+                                 float *dG, const int *mask, hipStream_t stream, int grid = 0) {
     int pl;
     bool rt;
     choose_opt<P, NT>(ka, pl, rt);
@@ -2039,7 +2049,8 @@ static hipError_t launch_score_t(const KArgs &ka, const uint8_t *seqs, int W, do
     }
     KArgs kb = ka;
     kb.opt = pl | (rt ? 4 : 0);
-    hipLaunchKernelGGL(k, dim3(W), dim3(NT), lds, stream, kb, kb.X, seqs, W, scores, terms, dG, mask);
+    hipLaunchKernelGGL(k, dim3(grid > 0 && grid < W ? grid : W), dim3(NT), lds, stream, kb, kb.X, seqs, W, scores,
+                       terms, dG, mask);
     return hipGetLastError();
 }
 
@@ -2145,9 +2156,12 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         if (e != hipSuccess) return e;
         KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state
         kf.tab = nullptr;
+        // overflows are rare: one block per CU scans the flags (ovf) instead of W
+        // blocks that mostly exit at once
+        constexpr int FB_GRID = 256;
         if (choose_p(ka) == 2)
-            return launch_score_t<ADX_NT2, 2, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
-        return launch_score_t<512, 1, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream);
+            return launch_score_t<ADX_NT2, 2, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream, FB_GRID);
+        return launch_score_t<512, 1, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream, FB_GRID);
     }
     switch (k) {
         case InsideK::MinPlusP2: return launch_score_t<ADX_NT2, 2, MinPlus>(ka, seqs, W, scores, terms, dG, mask, stream);
@@ -2319,7 +2333,7 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t s
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
         hipError_t e = launch_window(ka, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, st, s, nt_tot,
+        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 3) / 4), dim3(256), 0, stream, st, s, nt_tot,
                            ka.tab ? ka.cur_slot : nullptr, ka.tab ? ka.tab_valid : nullptr,
                            ka.mode == 1 ? ka.ovf : nullptr);
     }
