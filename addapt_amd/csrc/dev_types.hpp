@@ -186,6 +186,10 @@ struct KArgs {
     // waits for the outside pass (pair terms): score_kernel -> bppm_kernel
     // (re-using the inside tables just written) -> combine_kernel
     float *gstep;
+    // MC steps: the walkers in launch order, heaviest refold first (kernels.hip
+    // order_kernel; mfe_cells_kernel / pf_cells_kernel map blockIdx through it
+    // so the long folds do not trail the launch); null: blockIdx order
+    const int *order;
 };
 
 // Monte Carlo state (device, read/write).

@@ -2277,6 +2277,42 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
 }
 
+// Launch order of an MC step's folds: walkers whose proposal is scored, the
+// heaviest refold first (the band of cells containing a changed position,
+// about (m_hi + 2) (N - m_lo + 1); a fold from scratch counts as the whole
+// triangle), then the unscored ones (their blocks exit at once).  The folds'
+// durations vary by several times and the GPU starts workgroups in launch
+// order, so heavy folds no longer trail the launch.  64 weight classes, one
+// workgroup, LDS counters; the order within a class does not matter (each
+// walker's fold is independent of where it runs).
+__global__ void __launch_bounds__(1024) order_kernel(int W, const int *changed, const int *chg,
+                                                     const uint8_t *tab_valid, int Nraw, int *order) {
+    constexpr int NB = 65;   // 64 weight classes (0 = heaviest) + the unscored walkers
+    __shared__ int hist[NB], base[NB];
+    for (int k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const long long full = (long long)Nraw * Nraw;
+    auto bin_of = [&](int w) -> int {
+        if (changed[w] != 1) return NB - 1;
+        long long key = full;
+        if (tab_valid && tab_valid[w] && chg && chg[2 * w] >= 0)
+            key = (long long)(chg[2 * w + 1] + 2) * (Nraw - chg[2 * w] + 1);
+        const int b = int(min(full, max(0LL, key)) * 63 / (full > 0 ? full : 1));
+        return 63 - b;
+    };
+    for (int w = threadIdx.x; w < W; w += blockDim.x) atomicAdd(&hist[bin_of(w)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int k = 0; k < NB; k++) {
+            base[k] = acc;
+            acc += hist[k];
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < W; w += blockDim.x) order[atomicAdd(&base[bin_of(w)], 1)] = w;
+}
+
 // The score window of one MC step for the walkers flagged in `changed`: the
 // proposals' folds (prop_seq; incremental against the stored tables where
 // tab_valid allows), the outside pass when terms read base-pair probabilities,
@@ -2285,6 +2321,9 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
 static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *changed, double *tv,
                                 hipStream_t stream, hipEvent_t *evs) {
     if (evs) (void)hipEventRecord(evs[0], stream);
+    if (ka.order)
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, st.W, changed, ka.chg, ka.tab_valid, ka.Nraw,
+                           const_cast<int *>(ka.order));
     hipError_t e;
     if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
         // inside folds first (they write the proposal's tables), then the outside

@@ -408,7 +408,8 @@ __global__ void __launch_bounds__(PX_NT, 1)
 pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
                 float *gout) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int w = blockIdx.x / ka.n_groups2, grp = blockIdx.x % ka.n_groups2;
+    const int wb = blockIdx.x / ka.n_groups2, grp = blockIdx.x % ka.n_groups2;
+    const int w = (ka.order && wb < W) ? ka.order[wb] : wb;   // heaviest refolds first
     if (w >= W) return;
     if (mask && mask[w] != 1) return;
     const int vs0 = ka.groups2[2 * grp], vs1 = ka.groups2[2 * grp + 1];

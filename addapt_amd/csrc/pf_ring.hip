@@ -381,7 +381,8 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                float *gout, float *qscr) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ng = 2 * ka.n_groups2;
-    const int w = blockIdx.x / ng, rem = blockIdx.x % ng;
+    const int wb = blockIdx.x / ng, rem = blockIdx.x % ng;
+    const int w = (ka.order && wb < W) ? ka.order[wb] : wb;   // heaviest refolds first (kernels.hip order_kernel)
     const int grp = rem >> 1, half = rem & 1;
     if (w >= W) return;
     if (mask && mask[w] != 1) return;
