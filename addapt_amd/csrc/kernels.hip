@@ -2087,8 +2087,8 @@ hipError_t launch_pf_ring(const KArgs &ka, const uint8_t *seqs, int W, const int
                           float *qscr, hipStream_t stream);
 hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
                            hipStream_t stream);
-hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, double *scores, double *terms, float *dG,
-                            const int *mask, hipStream_t stream);
+hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, float *gout, const int *mask,
+                            hipStream_t stream);
 
 // MFE kernel choice, ADX_MFE_KERNEL (read at every launch, so a test can
 // switch it between contexts): cells (default) = mfe_cells_kernel (lanes =
@@ -2128,7 +2128,7 @@ static InsideK inside_choice(const KArgs &ka, bool has_g) {
 
 const char *inside_kernel_name(const KArgs &ka) {
     switch (inside_choice(ka, ka.gstep != nullptr)) {
-        case InsideK::MfeCells: return "mfe_cells_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
+        case InsideK::MfeCells: return "mfe_cells_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
         case InsideK::MfeRows16: return "score_kernel<" ADX_STR(ADX_NT16) ", 1, MinPlus16> + score_kernel<MinPlus> (FP32 fallback launch)";
         case InsideK::MinPlusP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, MinPlus>";
         case InsideK::MinPlus512: return "score_kernel<512, 1, MinPlus>";
@@ -2150,9 +2150,20 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         KArgs k16 = ka;
         k16.T = ka.T16;
         k16.X = ka.X16;
-        hipError_t e = k == InsideK::MfeCells
-                           ? launch_mfe_cells(k16, seqs, W, scores, terms, dG, mask, stream)
-                           : launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
+        hipError_t e;
+        if (k == InsideK::MfeCells) {
+            // one workgroup per (walker, fold group): energies to dG (or the gstep
+            // scratch), then the scores (the same arithmetic as combine_score)
+            if (!g) return hipErrorInvalidValue;
+            e = launch_mfe_cells(k16, seqs, W, g, mask, stream);
+            if (e != hipSuccess) return e;
+            KArgs kc = ka;
+            kc.gstep = g;
+            hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
+            e = hipGetLastError();
+        } else {
+            e = launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
+        }
         if (e != hipSuccess) return e;
         KArgs kf = ka;            // the FP32 fallback folds from scratch, keeps no state
         kf.tab = nullptr;
