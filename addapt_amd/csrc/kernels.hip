@@ -1246,12 +1246,7 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Lds<P> L;
     lds_layout<false, P>(smem, ka.cells, ka.Nmax, ka.n_variants, &L, ka.opt & 3, (ka.opt & 4) != 0, NT / WAVE);
-    // walkers blockIdx.x, + gridDim.x, ...: one each with a grid of W; the FP32
-    // refold of the few walkers whose 16-bit fold left the exact range runs on a
-    // short grid that scans the mask (launch_score_m)
-    for (int w = blockIdx.x; w < W; w += gridDim.x) {
-        if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
-        if (mask && mask[w] != 1) continue;  // MC: only walkers whose proposal changed
+    auto fold_one = [&](int w) {
         load_ctab(ka, L);
         for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
         __syncthreads();
@@ -1268,6 +1263,29 @@ score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, in
             }
         }
         __syncthreads();   // the LDS tables are the next walker's
+    };
+    if (int(gridDim.x) >= W) {   // one walker per workgroup
+        const int w = blockIdx.x;
+        if (SR::NV == 2 && ka.ovf && threadIdx.x == 0) ka.ovf[w] = 0;
+        if (mask && mask[w] != 1) return;  // MC: only walkers whose proposal changed
+        fold_one(w);
+        return;
+    }
+    // a short grid (the FP32 refold of the few walkers whose 16-bit fold left the
+    // exact range, launch_score_m): each workgroup scans its contiguous share of
+    // the mask 64 flags per load (every wave takes the same ballot) and folds
+    // the flagged walkers
+    const int per = (W + int(gridDim.x) - 1) / int(gridDim.x);
+    const int lo = int(blockIdx.x) * per, hi = min(W, lo + per);
+    const int lane = threadIdx.x & (WAVE - 1);
+    for (int base = lo; base < hi; base += WAVE) {
+        const int wl = base + lane;
+        uint64_t m = __ballot(wl < hi && (!mask || mask[wl] == 1));
+        while (m) {
+            const int q = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            fold_one(base + q);
+        }
     }
 }
 
