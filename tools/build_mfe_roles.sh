@@ -1,19 +1,31 @@
 #!/bin/bash
-# MFE block-partition variants: the 4-lanes-per-cell partition seeded with other
-# role costs (ADX_GEN_ROLES4) and/or the list role on another wave (MFE_LW).
-# usage: tools/build_mfe_roles.sh name/ROLES4/LW ...  -> addapt_amd/_lib/ablate/lib_mfe_<name>.so
+# MFE role / block-partition variants: the 4-lanes-per-cell partition seeded with
+# other role costs (ADX_GEN_ROLES4, "wave:cost,...") and mfe_cells.hip built with
+# extra flags (e.g. -DMFE_QW=7 puts q5 on the qm wave; "__" for spaces); every
+# other source from the tree.
+# usage: tools/build_mfe_roles.sh name/ROLES4/FLAGS ...  -> addapt_amd/_lib/ablate/lib_<name>.so
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
+SRC=$ROOT/addapt_amd/csrc
 OUT=$ROOT/addapt_amd/_lib/ablate
 mkdir -p $OUT
 T=$(mktemp -d)
+H="hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC"
+$H -c $SRC/adx_api.cpp -o $OUT/api.o &
+$H -c $SRC/energy.cpp -o $OUT/energy.o &
+for f in kernels.hip outside_cells.hip pf_cells.hip pf_ring.hip outside_ring.hip; do
+  $H -c $SRC/$f -o $OUT/tree_${f%.hip}.o &
+done
+wait
 for spec in "$@"; do
-  IFS=/ read -r name roles lw <<< "$spec"
+  IFS=/ read -r name roles flags <<< "$spec"
+  flags=${flags//__/ }
   (
-  mkdir -p $T/$name; cp $ROOT/addapt_amd/csrc/* $T/$name/
+  mkdir -p $T/$name; cp $SRC/* $T/$name/
   ADX_GEN_OUT=$T/$name ADX_GEN_ROLES4="$roles" python3 $ROOT/tools/gen_mfe_blocks.py 2>/dev/null
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC ${lw:+-DMFE_LW=$lw} -c $T/$name/mfe_cells.hip -o $OUT/c_mfe_$name.o
-  hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_mfe_$name.so $OUT/k_et.o $OUT/c_mfe_$name.o $OUT/o_et.o $OUT/p_et.o $OUT/r_et.o $OUT/q_et.o $OUT/api.o $OUT/energy.o
+  $H $flags -c $T/$name/mfe_cells.hip -o $OUT/${name}_mfe_cells.o
+  hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_$name.so $OUT/tree_kernels.o $OUT/${name}_mfe_cells.o \
+    $OUT/tree_outside_cells.o $OUT/tree_pf_cells.o $OUT/tree_pf_ring.o $OUT/tree_outside_ring.o $OUT/api.o $OUT/energy.o
   ) &
 done
 wait
