@@ -2187,7 +2187,10 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
         kf.tab = nullptr;
         // overflows are rare: one block per CU scans the flags (ovf) instead of W
         // blocks that mostly exit at once
-        constexpr int FB_GRID = 256;
+#ifndef ADX_FB_GRID
+#define ADX_FB_GRID 64
+#endif
+        constexpr int FB_GRID = ADX_FB_GRID;
         if (choose_p(ka) == 2)
             return launch_score_t<ADX_NT2, 2, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream, FB_GRID);
         return launch_score_t<512, 1, MinPlus>(kf, seqs, W, scores, terms, dG, ka.ovf, stream, FB_GRID);
@@ -2315,7 +2318,7 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
 // workgroup, LDS counters; the order within a class does not matter (each
 // walker's fold is independent of where it runs).
 __global__ void __launch_bounds__(1024) order_kernel(int W, const int *changed, const int *chg,
-                                                     const uint8_t *tab_valid, int Nraw, int *order) {
+                                                     const uint8_t *tab_valid, int Nraw, int *order, int *ovf) {
     constexpr int NB = 65;   // 64 weight classes (0 = heaviest) + the unscored walkers
     __shared__ int hist[NB], base[NB];
     for (int k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
@@ -2329,7 +2332,10 @@ __global__ void __launch_bounds__(1024) order_kernel(int W, const int *changed, 
         const int b = int(min(full, max(0LL, key)) * 63 / (full > 0 ? full : 1));
         return 63 - b;
     };
-    for (int w = threadIdx.x; w < W; w += blockDim.x) atomicAdd(&hist[bin_of(w)], 1);
+    for (int w = threadIdx.x; w < W; w += blockDim.x) {
+        atomicAdd(&hist[bin_of(w)], 1);
+        if (ovf) ovf[w] = 0;   // the 16-bit MFE folds' overflow flags (launch_mfe_cells skips its memset)
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
@@ -2352,7 +2358,7 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
     if (evs) (void)hipEventRecord(evs[0], stream);
     if (ka.order)
         hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, st.W, changed, ka.chg, ka.tab_valid, ka.Nraw,
-                           const_cast<int *>(ka.order));
+                           const_cast<int *>(ka.order), ka.mode == 1 ? ka.ovf : nullptr);
     hipError_t e;
     if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
         // inside folds first (they write the proposal's tables), then the outside
