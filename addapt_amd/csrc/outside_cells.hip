@@ -144,7 +144,13 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     L.mat = reinterpret_cast<uint8_t *>(smem + Y.MT);
     L.RL = Y.RL;
     L.NP = Y.NP;
+    // OX_WPERM (diagnostic builds): physical wave -> role, to try other role / SIMD pairings
+#ifdef OX_WPERM
+    constexpr int wperm[OX_NW] = {OX_WPERM};
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(wperm[tid / WAVE]);
+#else
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
+#endif
     const int C = Y.C, NP = Y.NP;
 #ifdef ADX_STAMP
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -309,7 +315,7 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     // cells of every diagonal in rank order (the B lanes; an unconstrained fold:
     // the pair type alone decides), on waves 2.. (neither touches G)
     if (wid >= 2) {
-        const int t2 = tid - 2 * WAVE, n2 = OX_NT - 2 * WAVE;
+        const int t2 = (wid - 2) * WAVE + lane, n2 = OX_NT - 2 * WAVE;
         for (int k = t2; k < OX_WIN * L.RL; k += n2) {
             L.qw[k] = 0.f;
             L.ow[k] = 0;

@@ -173,7 +173,13 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
     L.mat = reinterpret_cast<uint8_t *>(smem + Y.MT);
     L.RL = Y.RL;
     L.NP = Y.NP;
+    // OR_WPERM (diagnostic builds): physical wave -> role, to try other role / SIMD pairings
+#ifdef OR_WPERM
+    constexpr int wperm[OX_NW] = {OR_WPERM};
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(wperm[tid / WAVE]);
+#else
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
+#endif
     const int C = Y.C, NP = Y.NP;
     const DevTables &T = *ka.T;
 #ifdef ADX_STAMP
@@ -321,7 +327,7 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         }
     }
     if (wid >= 2) {
-        const int t2 = tid - 2 * WAVE, n2 = OX_NT - 2 * WAVE;
+        const int t2 = (wid - 2) * WAVE + lane, n2 = OX_NT - 2 * WAVE;
         for (int k = t2; k < OX_WIN * L.RL; k += n2) {
             L.qw[k] = 0.f;
             L.ow[k] = 0;

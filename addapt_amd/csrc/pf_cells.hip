@@ -46,7 +46,11 @@ constexpr int PX_NT = PX_NW * WAVE;
 // Roles of waves 7-13 (seven interior-loop waves, four qm waves: the qm wave
 // with the most items sets the step at a power-of-two lane split, so a fourth
 // qm wave halves it at about half of the spans; measured +1 % over 8 + 3).
-constexpr int PX_WF = 7, PX_WQ = 8, PX_WR = 9;   // F, Q, R
+#ifndef PX_ROLES
+#define PX_ROLES 7, 8, 9
+#endif
+constexpr int PX_ROLE_W[3] = {PX_ROLES};
+constexpr int PX_WF = PX_ROLE_W[0], PX_WQ = PX_ROLE_W[1], PX_WR = PX_ROLE_W[2];   // F, Q, R
 __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most items) or -1
     return w == 10 ? 0 : w == 11 ? 1 : w == 13 ? 2 : w == 12 ? 3 : (w >= 14 && w < PX_NW) ? w - 10 : -1;
 }

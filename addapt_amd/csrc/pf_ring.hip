@@ -423,7 +423,13 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     L.N = N;
     L.NP = Y.NP;
     L.RS = Y.RS;
+    // RG_WPERM (diagnostic builds): physical wave -> role, to try other role / SIMD pairings
+#ifdef RG_WPERM
+    constexpr int wperm[RG_NW] = {RG_WPERM};
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(wperm[tid / WAVE]);
+#else
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
+#endif
     const int C = Y.C, NP = Y.NP, RS = Y.RS;
     const DevTables &T = *ka.T;
 #ifdef ADX_STAMP

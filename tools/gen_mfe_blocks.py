@@ -81,9 +81,11 @@ def scost(u, S):
 
 
 # one-wave roles riding on block waves (mfe_cells.hip), in block-cost units,
-# from the stamps (tools/mfe_mc_stamps.py): finalize lane-set 0 on wave 6, q5
-# on wave 1, the qm1 column minima on wave 3, the list + records on wave 4
-ROLES4 = "6:8,1:7,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
+# from the stamps (tools/mfe_mc_stamps.py): finalize lane-set 0 on wave 1, the
+# qm1 column minima on wave 3, the list + records on wave 4 (q5 runs on the qm
+# wave 7, which has slack: 1.248M -> 1.266M MC steps/s; finalize on wave 1
+# instead of 6: +0.7-0.9 %; profiles/r04y_ab_roles.txt, r04z_ab_roles.txt)
+ROLES4 = "1:8,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
 
 
 def role_loads(S):
