@@ -144,13 +144,15 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
     L.mat = reinterpret_cast<uint8_t *>(smem + Y.MT);
     L.RL = Y.RL;
     L.NP = Y.NP;
-    // OX_WPERM (diagnostic builds): physical wave -> role, to try other role / SIMD pairings
-#ifdef OX_WPERM
+    // physical wave -> role: the finalize roles (0, 1) run on waves 2, 3 and the
+    // finalize-record roles (2, 3) on waves 0, 1, so the finalize shares its SIMDs
+    // with fewer multiloop-sum waves (config 3 462.5k -> 470.3k MC steps/s,
+    // profiles/r04zd_ab_wperm.txt; OX_WPERM overrides it in diagnostic builds)
+#ifndef OX_WPERM
+#define OX_WPERM 2, 3, 0, 1, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
+#endif
     constexpr int wperm[OX_NW] = {OX_WPERM};
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(wperm[tid / WAVE]);
-#else
-    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
-#endif
     const int C = Y.C, NP = Y.NP;
 #ifdef ADX_STAMP
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
