@@ -147,7 +147,7 @@ void build_tables(const EnergyParams &P, DevTables &T, bool mfe) {
 struct Motif {
     std::string seq, fold;
     double energy_kcal = 0.0;
-    int mode = ADX_MOTIF_ADD;
+    int mode = ADX_MOTIF_AUTO;   // the per-fold facade too: RNAfold's -9.22 holo MFE
     bool present = false;
 };
 
@@ -1454,19 +1454,49 @@ extern "C" adx_status adx_walkers_export(adx_ctx *c, void *dev_seqs, void *dev_s
     return ADX_OK;
 }
 
+// `a` waits (on the device) for the work queued on `b` so far
+static hipError_t stream_after(hipStream_t a, hipStream_t b) {
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(ev, b);
+    if (e == hipSuccess) e = hipStreamWaitEvent(a, ev, 0);
+    (void)hipEventDestroy(ev);
+    return e;
+}
+
+extern "C" adx_status adx_walkers_export_on(adx_ctx *c, void *dev_seqs, void *dev_scores, void *stream) {
+    if (!c) return fail(ADX_EINVAL, "adx_walkers_export_on: null context");
+    if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
+    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
+    const hipStream_t other = hipStream_t(stream);   // NULL: the null stream, a valid handle
+    // the caller's earlier reads of the buffers finish before the copies overwrite them
+    HIP_TRY(stream_after(c->pb.stream, other));
+    if (dev_seqs) HIP_TRY(hipMemcpyAsync(dev_seqs, c->cur_seq.p, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_scores)
+        HIP_TRY(hipMemcpyAsync(dev_scores, c->cur_score.p, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
+    // and the caller's later work on `stream` sees them
+    HIP_TRY(stream_after(other, c->pb.stream));
+    return ADX_OK;
+}
+
 extern "C" adx_status adx_walkers_import_after(adx_ctx *c, const void *dev_seqs, const void *dev_scores,
                                                void *producer_stream) {
     if (!c) return fail(ADX_EINVAL, "adx_walkers_import_after: null context");
-    if (producer_stream) {
-        // order the copies after the producer's queued writes (device-side wait, no host sync)
-        hipEvent_t ev;
-        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        hipError_t e = hipEventRecord(ev, hipStream_t(producer_stream));
-        if (e == hipSuccess) e = hipStreamWaitEvent(c->pb.stream, ev, 0);
-        (void)hipEventDestroy(ev);
-        HIP_TRY(e);
-    }
-    return adx_walkers_import(c, dev_seqs, dev_scores);
+    if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
+    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
+    // NULL is the null stream (torch's default stream), not "no producer": the
+    // engine stream is non-blocking and would not otherwise wait for it
+    const hipStream_t other = hipStream_t(producer_stream);
+    HIP_TRY(stream_after(c->pb.stream, other));
+    if (dev_seqs) HIP_TRY(hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_scores)
+        HIP_TRY(hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
+    if (dev_seqs && c->pb.dValid.p)   // new configurations: their next fold starts from scratch
+        HIP_TRY(hipMemsetAsync(c->pb.dValid.p, 0, W, c->pb.stream));
+    // the producer's later writes to the buffers wait for the copies
+    HIP_TRY(stream_after(other, c->pb.stream));
+    return ADX_OK;
 }
 
 extern "C" adx_status adx_walkers_import(adx_ctx *c, const void *dev_seqs, const void *dev_scores) {

@@ -229,7 +229,7 @@ void build_setup(const MonteCarlo &mc, DeviceConstPtr device, int g, EngineSetup
         d.aptamer_fold = e.apt_fold.c_str();
         d.aptamer_energy_kcal = kT() * std::log(a->affinity() / 1e6);
     }
-    d.motif_mode = ADX_MOTIF_ADD;   // one ligand model for PF and MFE folds
+    d.motif_mode = ADX_MOTIF_AUTO;   // ADD in partition functions, REPLACE in MFE folds (every reference pin)
     d.n_contexts = int(e.ctx.size());
     d.contexts = e.ctx.empty() ? nullptr : e.ctx.data();
     auto th = mc.thermostat();

@@ -17,7 +17,7 @@ DEFAULT_PARAMS = os.path.join(HERE, "data", "rna_turner2004_addapt.par")
 OK, EINVAL, EHIP, ECONSTRAINT, EPARAM, ENOMEM, EMOVE, ESTATE, ENODEV, EUNSUPPORTED = range(10)
 APO, HOLO = 0, 1
 THERMO_FIXED, THERMO_ANNEAL, THERMO_AUTO = 0, 1, 2
-MOTIF_ADD, MOTIF_REPLACE, MOTIF_AUTO = 0, 1, 2
+MOTIF_AUTO, MOTIF_ADD, MOTIF_REPLACE = 0, 1, 2   # include/addapt_gpu.h; AUTO is the default
 FOLD_PF, FOLD_MFE = 0, 1
 TERM_MACROSTATE, TERM_PAIR = 0, 1
 OUTCOMES = ["REJECT", "ACCEPT_WORSENED", "ACCEPT_UNCHANGED", "ACCEPT_IMPROVED"]
@@ -75,7 +75,7 @@ EXPORTS = [
     "adx_last_kernel_split_ms",
     "adx_last_kernel_names",
     "adx_walkers_download", "adx_score_batch", "adx_variant_desc", "adx_walkers_export",
-    "adx_walkers_import", "adx_walkers_import_after", "adx_set_temperature", "adx_bppm_batch",
+    "adx_walkers_import", "adx_walkers_import_after", "adx_walkers_export_on", "adx_set_temperature", "adx_bppm_batch",
     "adx_walkers_rescore",
 ]
 
@@ -114,6 +114,7 @@ def lib():
         L.adx_walkers_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_walkers_import.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_walkers_import_after.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.adx_walkers_export_on.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.adx_set_temperature.argtypes = [C.c_void_p, C.c_double]
         L.adx_walkers_download.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_double),
                                            C.POINTER(C.c_int64)]
@@ -228,7 +229,7 @@ class Engine:
     """
 
     def __init__(self, sequence, macrostates, terms, aptamer=None, thermostat=None, contexts=None,
-                 motif_mode=MOTIF_ADD, params=None, device=0, fold_mode="pf"):
+                 motif_mode=MOTIF_AUTO, params=None, device=0, fold_mode="pf"):
         self.params = params or default_params()
         self.N = len(sequence)
         d = RunDesc()
@@ -339,20 +340,29 @@ class Engine:
         _check(lib().adx_last_kernel_ms(self.ptr, C.byref(ms)))
         return ms.value
 
-    def export_walkers(self, dev_seqs_ptr, dev_scores_ptr):
+    def export_walkers(self, dev_seqs_ptr, dev_scores_ptr, on_stream=None):
         """Device-to-device copy of the walkers' sequence codes (W*N uint8) and
-        scores (W float64) into caller-owned device buffers (raw pointers)."""
-        _check(lib().adx_walkers_export(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+        scores (W float64) into caller-owned device buffers (raw pointers).
+        `on_stream` (a raw HIP stream handle, e.g.
+        torch.cuda.current_stream().cuda_stream -- 0 is the null stream) orders
+        the copy between that stream's earlier and later work without a host
+        synchronisation; None: synchronous."""
+        if on_stream is None:
+            _check(lib().adx_walkers_export(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
+        else:
+            _check(lib().adx_walkers_export_on(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr),
+                                               C.c_void_p(int(on_stream))))
 
     def import_walkers(self, dev_seqs_ptr, dev_scores_ptr, after_stream=None):
-        """Copy configurations back in; `after_stream` (a raw HIP stream handle,
-        e.g. torch.cuda.current_stream().cuda_stream) orders the copy after the
-        work queued there without a host synchronisation."""
+        """Copy configurations back in; `after_stream` (a raw HIP stream handle;
+        0 is the null stream, not "none") orders the copy after the work queued
+        there, and that stream's later work after the copy, without a host
+        synchronisation; None: the synchronous import."""
         if after_stream is None:
             _check(lib().adx_walkers_import(self.ptr, C.c_void_p(dev_seqs_ptr), C.c_void_p(dev_scores_ptr)))
         else:
             _check(lib().adx_walkers_import_after(self.ptr, C.c_void_p(dev_seqs_ptr),
-                                                  C.c_void_p(dev_scores_ptr), C.c_void_p(after_stream)))
+                                                  C.c_void_p(dev_scores_ptr), C.c_void_p(int(after_stream))))
 
     def set_temperature(self, t):
         _check(lib().adx_set_temperature(self.ptr, float(t)))

@@ -129,10 +129,11 @@ def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda"
     (tests, audits): called per round with host copies (round, partner, seqs,
     scores before, seqs, scores after the exchange).
 
-    Per round the host does no read-back of its own: the accept count stays a
-    device tensor (summed once after the last round), and the import is
-    ordered after the exchange's device work by a stream wait
-    (adx_walkers_import_after) instead of a device synchronisation."""
+    Per round the host does no read-back and no synchronisation of its own:
+    the accept count stays a device tensor (summed once after the last round),
+    and export and import are ordered against the exchange's device work on
+    torch's current stream by stream waits (adx_walkers_export_on /
+    adx_walkers_import_after; the null stream, handle 0, is a stream too)."""
     import torch
 
     engine.set_temperature(temps[rank])
@@ -146,13 +147,13 @@ def run(engine, dist, rank, world, steps, interval, temps, seed=0, device="cuda"
         engine.run_steps(k)
         done += k
         if done < steps or k == interval:
-            engine.export_walkers(seqs.data_ptr(), scores.data_ptr())
+            stream = torch.cuda.current_stream(seqs.device).cuda_stream if seqs.is_cuda else None
+            engine.export_walkers(seqs.data_ptr(), scores.data_ptr(), on_stream=stream)
             before = (seqs.cpu().numpy().copy(), scores.cpu().numpy().copy()) if observe else None
             a, b = exchange_round(dist, rnd, rank, world, temps, seqs, scores, seed)
             if observe:
                 observe(rnd, partner(rank, world, rnd), before[0], before[1],
                         seqs.cpu().numpy().copy(), scores.cpu().numpy().copy())
-            stream = torch.cuda.current_stream(seqs.device).cuda_stream if seqs.is_cuda else None
             engine.import_walkers(seqs.data_ptr(), scores.data_ptr(), after_stream=stream)
             att += a
             if b is not None:

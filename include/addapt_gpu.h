@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ADX_ABI_VERSION 3
+#define ADX_ABI_VERSION 4
 
 typedef enum adx_status {
     ADX_OK = 0,
@@ -123,14 +123,14 @@ typedef struct adx_thermostat {
     double t_init;
 } adx_thermostat;
 
-#define ADX_MOTIF_ADD 0        /* default, both fold modes: ligand bonus added to the motif
-                                  structure's own loop energies (one soft constraint for PF
-                                  and MFE, as vrna_sc_add_hi_motif is one call, scoring.cc:94;
-                                  pinned by the rhf(6) ensemble annotations, test_scoring.cc:54-55) */
-#define ADX_MOTIF_REPLACE 1    /* opt-in: motif structure's total energy := bonus */
-#define ADX_MOTIF_AUTO 2       /* opt-in: ADD in partition functions, REPLACE in MFE folds --
-                                  reproduces RNAfold's printed holo MFE -9.22
-                                  (test_scoring.cc:154) as well as the ensemble */
+#define ADX_MOTIF_AUTO 0       /* default (zero-initialised): ADD in partition functions,
+                                  REPLACE in MFE folds -- the convention that holds every
+                                  reference pin: the rhf(6) ensemble annotations and holo
+                                  classes (test_scoring.cc:54-55) and RNAfold's printed holo
+                                  MFE -9.22 (test_scoring.cc:152-154, tools/test_seq:9) */
+#define ADX_MOTIF_ADD 1        /* opt-in: ligand bonus added to the motif structure's own loop
+                                  energies in both fold modes (holo MFE of THEO: -10.92) */
+#define ADX_MOTIF_REPLACE 2    /* opt-in: motif structure's total energy := bonus, both modes */
 
 #define ADX_FOLD_PF 0          /* MacrostateProbTerm over vrna_pf ensembles (scoring.cc:53-71) */
 #define ADX_FOLD_MFE 1         /* the same terms over minimum free energies:
@@ -151,7 +151,7 @@ typedef struct adx_run_desc {
     const char *aptamer_seq;         /* NULL: no aptamer (holo folds like apo) */
     const char *aptamer_fold;
     double aptamer_energy_kcal;      /* kT*ln(Kd/1M) (scoring.cc:91-99) */
-    int motif_mode;                  /* ADX_MOTIF_ADD (default, 0) / _REPLACE / _AUTO */
+    int motif_mode;                  /* ADX_MOTIF_AUTO (default, 0) / _ADD / _REPLACE */
     int n_contexts;                  /* 0 = none; else map (name) order */
     const adx_context_desc *contexts;
     adx_thermostat thermostat;
@@ -220,7 +220,12 @@ adx_status adx_walkers_download(adx_ctx *ctx, char *seqs, double *scores, int64_
  * fresh scores[W] (and term_values[W*n_terms*max(1,n_contexts)], optional).
  * The stored scores are left alone: a caller compares the two to check that
  * incremental refolds equal scratch folds bit for bit.  adx_walkers_init
- * computes the walkers' first scores this way (sampling.cc:40). */
+ * computes the walkers' first scores this way (sampling.cc:40).
+ * State the call overwrites: each walker's table slot pointer (cur_slot flips
+ * to the fresh tables) and valid byte (set), the proposal buffers of the last
+ * step (proposed sequences and scores, changed flags, the launch-order list)
+ * and, with base-pair terms, the pair-probability and per-variant energy
+ * scratch -- so read a step's proposals before rescoring. */
 adx_status adx_walkers_rescore(adx_ctx *ctx, double *scores, double *term_values);
 
 /* Replica exchange (BASELINE config 5): copy the walkers' configurations --
@@ -228,17 +233,23 @@ adx_status adx_walkers_rescore(adx_ctx *ctx, double *scores, double *term_values
  * from caller-owned DEVICE buffers on the context's GPU (e.g. torch tensors
  * swapped between ranks over RCCL).  RNG streams, counters and thermostat
  * state stay with the walker slot: a swap moves configurations between
- * temperatures.  Synchronous; the caller's own writes to the buffers must be
- * complete (its stream synchronized) before adx_walkers_import.  An imported
- * walker folds from scratch until one of its proposals is accepted; from then
- * on it refolds incrementally on that proposal's tables. */
+ * temperatures.  An imported walker folds from scratch until one of its
+ * proposals is accepted; from then on it refolds incrementally on that
+ * proposal's tables.
+ *
+ * adx_walkers_export / adx_walkers_import are synchronous: export returns with
+ * the buffers written; the caller's own writes to the buffers must be complete
+ * (its stream synchronized) before adx_walkers_import. */
 adx_status adx_walkers_export(adx_ctx *ctx, void *dev_seqs, void *dev_scores);
 adx_status adx_walkers_import(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores);
-/* adx_walkers_import ordered after the work already queued on the caller's
- * HIP stream `producer_stream` (e.g. torch's current stream holding the
- * exchange's copies): the context's stream waits on an event recorded there,
- * so the caller needs no host synchronisation before the import.  NULL = the
- * plain import. */
+/* Stream-ordered forms, no host synchronisation: `stream` / `producer_stream`
+ * is the caller's HIP stream that reads / writes the buffers (e.g. torch's
+ * current stream; NULL is the null stream -- a valid stream, not "none").
+ * The copies run on the context's stream after the work already queued on the
+ * caller's stream, and the caller's stream waits for the copies before its
+ * later work (so it may read the exported buffers, and overwrite the imported
+ * ones, right away).  Use the synchronous pair above for "no stream". */
+adx_status adx_walkers_export_on(adx_ctx *ctx, void *dev_seqs, void *dev_scores, void *stream);
 adx_status adx_walkers_import_after(adx_ctx *ctx, const void *dev_seqs, const void *dev_scores,
                                     void *producer_stream);
 /* Temperature of an ADX_THERMO_FIXED context (one rung of a replica ladder). */

@@ -72,11 +72,12 @@ void orc_params_free(orc_params *P);
 const char *orc_last_error(void);
 
 /* ---- folding ---------------------------------------------------------- */
-/* Ligand motif (vrna_sc_add_hi_motif, scoring.cc:92-100).  mode 0 = "add"
- * (bonus added to the motif structure's intrinsic energy), mode 1 =
- * "replace" (motif structure's total energy := bonus), mode 2 = "auto"
- * (add in partition functions, replace in the MFE: the conventions the
- * reference's RNAfold annotations pin, test_scoring.cc:52-55 and :154). */
+/* Ligand motif (vrna_sc_add_hi_motif, scoring.cc:92-100).  mode 0 = "auto"
+ * (the default: add in partition functions, replace in the MFE -- the
+ * conventions the reference's RNAfold annotations pin, test_scoring.cc:52-55
+ * and :154), mode 1 = "add" (bonus added to the motif structure's intrinsic
+ * energy), mode 2 = "replace" (motif structure's total energy := bonus);
+ * the numbering of the engine's ADX_MOTIF_*. */
 typedef struct orc_motif {
     const char *seq;     /* upper case ACGU */
     const char *fold;    /* dot-bracket, outer pair spans the motif */

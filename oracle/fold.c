@@ -257,13 +257,13 @@ static int model_init(model_t *m, const orc_params *P, const char *seq, const ch
         free(stk);
         double eint = orc_eval_structure(P, motif->seq, motif->fold); /* kcal */
         m->m_Eint = eint;
-        /* mode 0 (ADD, the default): bonus + the motif's own loops in both fold
-         * modes (the ensemble annotations, test_scoring.cc:54-55); mode 1
-         * (REPLACE): motif energy := bonus; mode 2 (AUTO, opt-in): ADD for
-         * partition functions, REPLACE for the MFE -- also reproduces the printed
-         * holo MFE -9.22 (test_scoring.cc:154) */
-        double beff = motif->mode == 1 ? motif->energy_kcal - eint : motif->energy_kcal;
-        double beff_mfe = motif->mode == 0 ? motif->energy_kcal : motif->energy_kcal - eint;
+        /* mode 0 (AUTO, the default): ADD for partition functions (bonus + the
+         * motif's own loops: the ensemble annotations, test_scoring.cc:54-55),
+         * REPLACE for the MFE (motif energy := bonus: the printed holo MFE
+         * -9.22, test_scoring.cc:152-154); mode 1 (ADD) and mode 2 (REPLACE)
+         * apply one reading to both fold modes */
+        double beff = motif->mode == 2 ? motif->energy_kcal - eint : motif->energy_kcal;
+        double beff_mfe = motif->mode == 1 ? motif->energy_kcal : motif->energy_kcal - eint;
         m->m_extra = boltz(eint * 100.0) * (boltz(beff * 100.0) - 1.0);
         m->m_beff = beff;
         m->m_mfe_dcal = (int)lround(100.0 * (eint + beff_mfe));

@@ -153,8 +153,12 @@ def default_params():
     return _default_params
 
 
-def make_motif(seq, fold, energy_kcal, mode=0):
-    """mode 0 = ADD (default, as the engine), 1 = REPLACE, 2 = AUTO (ADD in PF, REPLACE in MFE)."""
+MOTIF_AUTO, MOTIF_ADD, MOTIF_REPLACE = 0, 1, 2   # the engine's ADX_MOTIF_* numbering
+
+
+def make_motif(seq, fold, energy_kcal, mode=MOTIF_AUTO):
+    """mode MOTIF_AUTO (0, default as the engine: ADD in PF, REPLACE in MFE),
+    MOTIF_ADD (1), MOTIF_REPLACE (2)."""
     m = Motif(_b(seq), _b(fold), energy_kcal, mode)
     m._keep = (seq, fold)
     return m

@@ -111,19 +111,23 @@ def test_fold_mfe_motif(native, oracle):
             assert _same(g, oracle.mfe_energy(seq, cst, m)), (seq, g)
 
 
-@pytest.mark.parametrize("mode", ["replace", "auto", "add"])
+@pytest.mark.parametrize("mode", ["replace", "auto", "add", "default"])
 def test_engine_holo_mfe_motif_modes(native, oracle, mode):
     """The engine's MFE holo fold of the THEO aptamer under each motif mode
     (adx_run_desc.motif_mode): REPLACE and AUTO give RNAfold's printed holo
-    MFE -9.22 kcal/mol with the -9.22 bonus (test_scoring.cc:154), ADD (the
-    default) adds the motif's own loop energies (-10.92); every mode equals
-    the oracle's fold under the same mode."""
+    MFE -9.22 kcal/mol with the -9.22 bonus (test_scoring.cc:154), the opt-in
+    ADD adds the motif's own loop energies (-10.92); every mode equals the
+    oracle's fold under the same mode.  "default" leaves motif_mode at its
+    zero-initialised value, which must be AUTO."""
     apt, fold = workloads.THEO_SEQ, workloads.THEO_FOLD
-    mm = {"add": native.MOTIF_ADD, "replace": native.MOTIF_REPLACE, "auto": native.MOTIF_AUTO}[mode]
-    om = {"add": 0, "replace": 1, "auto": 2}[mode]
+    mm = {"add": native.MOTIF_ADD, "replace": native.MOTIF_REPLACE, "auto": native.MOTIF_AUTO}.get(mode)
+    om = {"add": oracle.MOTIF_ADD, "replace": oracle.MOTIF_REPLACE}.get(mode, oracle.MOTIF_AUTO)
     terms = [("apo", 0, False, 1.0), ("holo", 0, True, 1.0)]
-    eng = native.Engine(apt, ["." * len(apt)], terms, aptamer=(apt, fold, -9.22), motif_mode=mm,
+    kw = {} if mm is None else {"motif_mode": mm}
+    eng = native.Engine(apt, ["." * len(apt)], terms, aptamer=(apt, fold, -9.22), **kw,
                         fold_mode="mfe", thermostat=native.make_thermostat("fixed", t=1.0))
+    if mm is None:
+        assert eng._desc.motif_mode == native.MOTIF_AUTO == 0
     _, _, dg = eng.score_batch([apt])
     holo = [v for v in range(eng.info.n_variants) if eng.variant(v)[1] == 1 and eng.variant(v)[2] < 0]
     assert holo

@@ -43,7 +43,7 @@ def _motif_forced(seq, o):
 def test_mfe_with_motif_is_min_over_occurrences(oracle, N):
     seq, _ = workloads.synthetic(N)
     seq = seq.upper()
-    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus(), oracle.MOTIF_ADD)
     occ = [o for o in range(len(seq) - 26) if seq[o:o + 27] == workloads.THEO_SEQ]
     assert occ
     expect = oracle.mfe_energy(seq)
@@ -54,7 +54,7 @@ def test_mfe_with_motif_is_min_over_occurrences(oracle, N):
 
 def test_mfe_theo_holo(oracle):
     seq = workloads.THEO_SEQ
-    m = oracle.make_motif(seq, workloads.THEO_FOLD, oracle.theo_bonus(), 0)
+    m = oracle.make_motif(seq, workloads.THEO_FOLD, oracle.theo_bonus(), oracle.MOTIF_ADD)
     e_motif = oracle.eval_structure(seq, workloads.THEO_FOLD)
     assert oracle.mfe_energy(seq, None, m) == pytest.approx(
         min(oracle.mfe_energy(seq), e_motif + _bonus_dcal(oracle)), abs=1e-6)
@@ -69,3 +69,16 @@ def test_constrained_mfe_is_bounded_by_free(oracle, N):
     assert act >= free - 1e-9
     e, s = oracle.mfe(seq, cst)
     assert act == pytest.approx(e, abs=1e-9)
+
+
+@pytest.mark.parametrize("N", [60, 100])
+def test_default_motif_mode_is_auto(oracle, N):
+    """The oracle's default motif convention (AUTO, as the engine's): REPLACE in
+    MFE folds, ADD in partition functions."""
+    seq, _ = workloads.synthetic(N)
+    seq = seq.upper()
+    b = oracle.theo_bonus()
+    mk = lambda *mode: oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, b, *mode)
+    assert oracle.mfe_energy(seq, None, mk()) == oracle.mfe_energy(seq, None, mk(oracle.MOTIF_REPLACE))
+    assert oracle.pf_energy(seq, None, mk()) == oracle.pf_energy(seq, None, mk(oracle.MOTIF_ADD))
+    assert oracle.mfe_energy(seq, None, mk()) > oracle.mfe_energy(seq, None, mk(oracle.MOTIF_ADD))

@@ -116,7 +116,7 @@ class _HostEngine:
     def run_steps(self, k):
         self.steps += k
 
-    def export_walkers(self, seqs_ptr, scores_ptr):
+    def export_walkers(self, seqs_ptr, scores_ptr, on_stream=None):
         import ctypes
 
         ctypes.memmove(seqs_ptr, self.seqs.data_ptr(), self.W * self.N)

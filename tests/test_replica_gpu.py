@@ -177,3 +177,74 @@ def test_config5_ladder_at_workload():
     for rank in (0, 1):
         assert res[rank][3] <= 1.0, res[rank][3]
         assert sum(res[rank][4]) == W * 15
+
+
+def _rung_stream_ordered(rank, world, port, q):
+    """One exchange round with observe=None: the export / import are ordered
+    against the exchange by stream waits only (no host sync in replica.run)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from addapt_amd import native, replica
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, N, steps = 512, 100, 6
+        tmpl, active = workloads.synthetic(N)
+        apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+        temps = replica.ladder_temperatures(world)
+        ids = list(range(rank * W, (rank + 1) * W))
+        init = workloads.walker_sequences(tmpl, [active], W, seed_base=1000 + ids[0])
+
+        def engine():
+            e = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt,
+                              thermostat=native.make_thermostat("fixed", t=temps[rank]), fold_mode="mfe")
+            e.walkers_init(ids, init)
+            return e
+
+        # the pre-swap configurations: the same walkers (same seeds, temperature) run alone
+        twin = engine()
+        twin.run_steps(steps)
+        pre_seqs, pre_scores, _ = twin.download()
+        del twin
+        eng = engine()
+        stats = replica.run(eng, dist, rank, world, steps=steps, interval=steps, temps=temps, seed=5)
+        seqs, scores, _ = eng.download()
+        fresh, _ = eng.rescore()
+        q.put((rank, stats, pre_seqs, pre_scores.tolist(), seqs, scores.tolist(), fresh.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_stream_ordered_exchange_without_observe():
+    """replica.run with observe=None on CUDA (the timed bench path).
+    Every walker's stored score equals a from-scratch fold of its stored
+    sequence bit for bit (no half-swapped walker), and slot by slot the pair's
+    configurations after the round are the two pre-swap ones."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rung_stream_ordered, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=600)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    r0, r1 = res[0], res[1]
+    assert r0[1]["rounds"] == r1[1]["rounds"] == 1
+    swapped = 0
+    for rank in (0, 1):
+        _, _, _, _, seqs, scores, fresh = res[rank]
+        assert scores == fresh      # bit for bit: each stored score belongs to its sequence
+    for w in range(len(r0[4])):
+        before = sorted([(r0[2][w], r0[3][w]), (r1[2][w], r1[3][w])])
+        after = sorted([(r0[4][w], r0[5][w]), (r1[4][w], r1[5][w])])
+        assert before == after, w
+        swapped += r0[4][w] != r0[2][w]
+    assert swapped > 0
+    assert swapped <= r0[1]["accepted"] == r1[1]["accepted"]

@@ -3,8 +3,9 @@
 
 The five RNAfold annotations (test_scoring.cc:52-55, 86-87, 152-154) and the
 macrostate / base-pair-probability thresholds (test_scoring.cc:83-259), for
-a parameter file (default: the shipped one) and a motif mode (default ADD = 0,
-the engine's default; 2 = AUTO: ADD in partition functions, REPLACE in the MFE),
+a parameter file (default: the shipped one) and a motif mode (default AUTO = 0,
+the engine's default: ADD in partition functions, REPLACE in the MFE; 1 = ADD,
+2 = REPLACE),
 plus the 204 per-position ensemble classes of rhf(6) (test_scoring.cc:54-55,
 tests/pseudo_bracket.py).  The holo aptamer MFE annotation -9.22 is RNAfold's
 MFE under the REPLACE reading; it is reported for REPLACE and, as information,
@@ -39,7 +40,7 @@ def main():
     ann("hairpin MFE " + s, e, -2.20)
     e, s = O.mfe(workloads.THEO_SEQ, params=P)
     ann("THEO apo MFE " + s, e, -6.20)
-    theo_rep = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), 1)
+    theo_rep = O.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, O.theo_bonus(), O.MOTIF_REPLACE)
     ann("THEO holo MFE (REPLACE)", O.mfe_energy(workloads.THEO_SEQ, None, theo_rep, params=P), -9.22)
     info = [("THEO holo MFE (mode %d)" % mode, O.mfe_energy(workloads.THEO_SEQ, None, theo, params=P), -9.22)]
     ann("rhf(6) apo ensemble", O.pf_energy(rhf, params=P), -29.58)
