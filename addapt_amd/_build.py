@@ -17,7 +17,7 @@ OBJ = os.path.join(OUT, "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-GPU_SOURCES = ["kernels.hip", "mfe_cells.hip", "outside_cells.hip", "pf_cells.hip", "pf_ring.hip", "outside_ring.hip", "adx_api.cpp",
+GPU_SOURCES = ["kernels.hip", "mfe_cells.hip", "mfe_pair.hip", "outside_cells.hip", "pf_cells.hip", "pf_ring.hip", "outside_ring.hip", "adx_api.cpp",
                "energy.cpp"]
 
 

@@ -2107,6 +2107,7 @@ hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const in
                            hipStream_t stream);
 hipError_t launch_mfe_cells(const KArgs &ka, const uint8_t *seqs, int W, float *gout, const int *mask,
                             hipStream_t stream);
+bool mfe_pair_active(const KArgs &ka);
 
 // MFE kernel choice, ADX_MFE_KERNEL (read at every launch, so a test can
 // switch it between contexts): cells (default) = mfe_cells_kernel (lanes =
@@ -2146,7 +2147,13 @@ static InsideK inside_choice(const KArgs &ka, bool has_g) {
 
 const char *inside_kernel_name(const KArgs &ka) {
     switch (inside_choice(ka, ka.gstep != nullptr)) {
-        case InsideK::MfeCells: return "mfe_cells_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
+        case InsideK::MfeCells: {
+            KArgs k16 = ka;
+            k16.T = ka.T16;
+            k16.X = ka.X16;
+            return mfe_pair_active(k16) ? "mfe_pair_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)"
+                                        : "mfe_cells_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
+        }
         case InsideK::MfeRows16: return "score_kernel<" ADX_STR(ADX_NT16) ", 1, MinPlus16> + score_kernel<MinPlus> (FP32 fallback launch)";
         case InsideK::MinPlusP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, MinPlus>";
         case InsideK::MinPlus512: return "score_kernel<512, 1, MinPlus>";

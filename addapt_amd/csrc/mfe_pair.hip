@@ -1,0 +1,929 @@
+// gfx950 minimum-free-energy fold for the Monte Carlo score (BASELINE
+// configs[1]) with TWO anti-diagonals per barrier.  The recursion, the tables
+// and the lanes = cells mapping are those of mfe_cells.hip (Zuker MFE of the
+// ViennaRNA-2.x default model, dangles = 2, hard constraints, ligand motif;
+// oracle/fold.c orc_mfe_energy; apo | holo packed as 16-bit halves); what
+// changes is the step's dependency structure, so that one barrier serves two
+// diagonals and a B lane-set holds the pairable cells of both:
+//
+// Step d (d = 6, 8, ...; one barrier at its end):
+//   F  finalize e0 = d-2 and e1 = d-1, lanes = rows i, two cells per lane:
+//      c = min(B's partials (loop sizes u >= 2), the stack and bulge-1 shapes
+//      (inner spans e-2, e-3: final a step earlier), hairpin / motif,
+//      multiloop closing mla(i+1, j-1) + closing), qbm = c + mismatchI,
+//      qm1 = min(c + stem, qm1(i, j-1) + MLbase) (cell e1 takes cell e0's qm1
+//      from the same lane), the unpaired part of qm
+//      U(i, j) = min(qm1(i, j), U(i+1, j) + MLbase) (cell e1 takes U of row
+//      i+1 from the next lane), qm = min(split, U)
+//   B  interior-loop partials of diagonals d and d+1, loop sizes u >= 2
+//      (inner spans <= d-3: final a step earlier), one lane-set over the
+//      pairable cells of both; every block wave folds its partial into the
+//      cell's slot with an LDS atomic min (apo and holo halves apart)
+//   M  split parts of qm for spans d, d+1 (they read spans <= d-4)
+//   Q  q5[d-3] and q5[d-2] in one pass over k
+//   L  the pairable cells of diagonals d+2, d+3 and their B records
+// Everything a phase reads was written one step earlier or before the loop,
+// so the 97 diagonals of a 100-nt fold take 49 barriers instead of 97, and the
+// step's fixed costs (records, counts, the B cell setup, the roles' round
+// trips) are paid once per two diagonals.
+//
+// Every stored value goes through pfin() as in mfe_cells.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dev_types.hpp"
+#include "fold_common.hpp"
+#include "mfe_common.hpp"
+
+namespace adx {
+
+#ifdef ADX_STAMP
+__device__ unsigned long long g_stamps_p[16][16];
+#define PSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
+
+namespace {
+
+// waves per walker: 0..6 interior-loop blocks, 7 the split parts of qm; the
+// finalize, list and q5 roles ride on block waves (two workgroups per CU)
+constexpr int NWV = 8;
+constexpr int MA_WAVE = 7;
+constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
+
+#include "mfe_pair_blocks.inc"
+static_assert(MFE_NBLK == 7, "seven block waves");
+
+constexpr int PINF = 32767;   // an impossible half, sign-extended (the partial slots)
+
+// ---------------------------------------------------------------- LDS carve
+struct CP {
+    u32 *qbm, *qm, *qm1;   // cell tables (fold_common.hpp indexing); qbm has an
+                           // impossible "span 3" diagonal right before it
+    int *part;             // [4][2][np]: B's partial minima of a diagonal (span & 3) by row,
+                           //   apo / holo halves sign-extended (ds_min_i32)
+    u32 *mla;              // [6][np]: split part of qm by span % 6, by row
+    u32 *colmin;           // [4][np]: U(j - span, j) by span & 3, by column j
+    u32 *q5;               // [np]
+    u32 *ct;               // CT_SIZE (DevScaled::ctab, packed)
+    u32 *dt;               // DT_* block (packed)
+    uint8_t *cc;           // inner-pair code per cell (diagonal-major), pad before it
+    uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
+    uint8_t *cl;           // [2][2 np]: rows of the pairable cells of a step's two diagonals, by step parity
+    int *cnt;              // [2][2]: cells of the step's first diagonal, of both
+    u32 *rec;              // [2][3][64]: the B cells' setup (rank < 64 over both diagonals) by step parity
+    u32 *e4;               // [MFE_E4_SLOTS][4]: per-slice generic energies of the 4-lane blocks
+    int np;
+};
+
+constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
+constexpr int MFE_E4_MAX = 64;
+template <int NM>
+struct PLay {
+    static constexpr int NP = NM + 2;
+    static constexpr size_t C = size_t(NM - 4) * (NM - 3) / 2;
+    static constexpr size_t PADQ = al16(size_t(NM - 3) * 4);   // the span-3 diagonal of qbm (impossible)
+    static constexpr size_t QBM = PADQ;
+    static constexpr size_t QM = QBM + al16(C * 4);
+    static constexpr size_t QM1 = QM + al16(C * 4);
+    static constexpr size_t PART = QM1 + al16(C * 4);          // PART, MLA, CMN: the setup's scratch too
+    static constexpr size_t MLA = PART + al16(4 * 2 * NP * 4);
+    static constexpr size_t CMN = MLA + al16(6 * NP * 4);
+    static constexpr size_t Q5 = CMN + al16(4 * NP * 4);
+    static constexpr size_t CT = Q5 + al16(NP * 4);
+    static constexpr size_t DT = CT + al16(CT_SIZE * 4);
+    static constexpr size_t CC = DT + al16(size_t(DT_HP) * 4) + al16(NM - 3);   // span-3 codes before it
+    static constexpr size_t BY = CC + al16(C);
+    static constexpr size_t CLS = BY + al16(8 * NP);
+    static constexpr size_t CNT = CLS + al16(4 * NP);
+    static constexpr size_t REC = CNT + 16;
+    static constexpr size_t E4 = REC + 2 * 3 * 64 * 4;
+    static constexpr size_t BYTES = E4 + size_t(MFE_E4_MAX) * 16;
+    __device__ static CP carve(char *b) {
+        CP l;
+        l.qbm = reinterpret_cast<u32 *>(b + QBM);
+        l.qm = reinterpret_cast<u32 *>(b + QM);
+        l.qm1 = reinterpret_cast<u32 *>(b + QM1);
+        l.part = reinterpret_cast<int *>(b + PART);
+        l.mla = reinterpret_cast<u32 *>(b + MLA);
+        l.colmin = reinterpret_cast<u32 *>(b + CMN);
+        l.q5 = reinterpret_cast<u32 *>(b + Q5);
+        l.ct = reinterpret_cast<u32 *>(b + CT);
+        l.dt = reinterpret_cast<u32 *>(b + DT);
+        l.cc = reinterpret_cast<uint8_t *>(b + CC);
+        uint8_t *y = reinterpret_cast<uint8_t *>(b + BY);
+        l.S = y;
+        l.up = y + NP;
+        l.dn = y + 2 * NP;
+        l.ptn = y + 3 * NP;
+        l.enc = y + 4 * NP;
+        l.flg = y + 5 * NP;
+        l.mat = y + 6 * NP;
+        l.raw = y + 7 * NP;
+        l.cl = reinterpret_cast<uint8_t *>(b + CLS);
+        l.cnt = reinterpret_cast<int *>(b + CNT);
+        l.rec = reinterpret_cast<u32 *>(b + REC);
+        l.e4 = reinterpret_cast<u32 *>(b + E4);
+        l.np = NP;
+        return l;
+    }
+};
+static_assert(MFE_E4_SLOTS <= MFE_E4_MAX, "CP::e4 holds the generated slots");
+
+struct IncM {
+    const u32 *src;
+    u32 *dst;
+    int m_lo, m_hi;
+};
+
+__device__ __forceinline__ int lanesets(int n) { return (n + 63) >> 6; }
+__device__ __forceinline__ int sext_lo(u32 x) { return int(short(x & 0xFFFFu)); }
+__device__ __forceinline__ int sext_hi(u32 x) { return int(x) >> 16; }
+__device__ __forceinline__ u32 pack2(int lo, int hi) { return (u32(lo) & 0xFFFFu) | (u32(hi) << 16); }
+
+template <int NT, int NM>
+__device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *__restrict__ XS,
+                                              const DevTables *__restrict__ TT, const int *vs, const uint8_t *raw,
+                                              const CP &L, u32 &z, bool &bad, const IncM &inc) {
+    static_assert(NT == NWV * WAVE, "one wave per block slot");
+    const DevVariant V = ka.variants[vs[0]];
+    const bool mh0 = ka.variants[vs[0]].motif != 0, mh1 = ka.variants[vs[1]].motif != 0;
+    const int N = uni(V.N);
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    const int wid = uni(tid / WAVE);
+    const int NP = L.np;
+    const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
+#ifdef ADX_STAMP
+    const unsigned long long st_setup0 = __builtin_amdgcn_s_memtime();
+#endif
+    const bool incr = inc.src != nullptr;
+    const int m_lo = uni(inc.m_lo), m_hi = uni(inc.m_hi);
+    // changed rows of span dd (cells containing a changed position; mfe_cells.hip)
+    auto clo = [&](int dd) { return incr ? max(1, m_lo - 1 - dd) : 1; };
+    auto chi = [&](int dd) { return incr ? min(N - dd, m_hi + 1) : N - dd; };
+    auto qlo = [&](int s) { return incr ? max(1, m_lo - 2 - s) : 1; };
+    auto qhi = [&](int s) { return incr ? min(N - s, m_hi + 2) : N - s; };
+
+    // ---- refold restore first (8-byte vector loads)
+    if (incr) {
+        const size_t Cs = size_t(ka.cells);
+        const int C = ((N - 4) * (N - 3)) >> 1, half = C >> 1;
+#pragma unroll 8
+        for (int k = tid; k < 3 * half; k += NT) {
+            const int a = k / half, c = k - a * half;
+            const uint2 x = *reinterpret_cast<const uint2 *>(inc.src + a * Cs + 2 * c);
+            u32 *d = a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1;
+            *reinterpret_cast<uint2 *>(d + 2 * c) = x;
+        }
+        if (C & 1)
+            for (int a = tid; a < 3; a += NT) (a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1)[C - 1] = inc.src[a * Cs + C - 1];
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) L.q5[k] = inc.src[3 * Cs + k];
+    }
+    // setup scratch in the partial / split / U slots (first written after the per-cell pass)
+    uint32_t *spk = reinterpret_cast<uint32_t *>(L.part);
+    u32 *spv = spk + MAX_SPECIAL_HP;
+    uint8_t *mcode = reinterpret_cast<uint8_t *>(spk + 2 * MAX_SPECIAL_HP);
+    int8_t *mpt = reinterpret_cast<int8_t *>(mcode + MAX_MOTIF);
+    static_assert(2 * MAX_SPECIAL_HP * 4 + 2 * MAX_MOTIF <= PLay<NM>::MLA - PLay<NM>::PART, "setup tables fit the partials");
+    for (int k = tid; k < MAX_SPECIAL_HP; k += NT) {
+        const bool on = k < XS->n_special;
+        spk[k] = on ? XS->sp_key[k] : 0xFFFFFFFFu;
+        spv[k] = on ? __float_as_uint(XS->sp_val[k]) : INF16;
+    }
+    for (int k = tid; k < MAX_MOTIF; k += NT) {
+        mcode[k] = XS->motif_code[k];
+        mpt[k] = XS->motif_pt[k];
+    }
+    for (int k = tid; k < NM - 3; k += NT) {   // the impossible span-3 diagonal (B's d-lanes reach it)
+        (L.qbm - (NM - 3))[k] = INF16;
+        (L.cc - (NM - 3))[k] = 0;
+    }
+
+    // ---- sequence, constraint arrays, motif sites (mfe_cells.hip)
+    const uint8_t *cons = ka.cons + V.cons_off;
+    const int np = N + 2;
+    const uint8_t *bef = nullptr, *aft = nullptr;
+    int blen = 0;
+    if (V.ctx >= 0) {
+        bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
+        blen = ka.ctx_off[4 * V.ctx + 1];
+        aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
+    }
+    bool constrained = false;
+    for (int k = tid; k < np; k += NT) {
+        uint8_t s = 0;
+        if (k >= 1 && k <= N) {
+            const int pp = k - 1;
+            if (pp < blen) s = bef[pp];
+            else if (pp < blen + ka.Nraw) s = raw[pp - blen];
+            else s = aft[pp - blen - ka.Nraw];
+        }
+        L.S[k] = s;
+        const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k];
+        L.up[k] = cons[k];
+        L.dn[k] = cons[np + k];
+        L.ptn[k] = pt;
+        L.enc[k] = cons[3 * np + k];
+        L.flg[k] = f;
+        L.mat[k] = 0;
+        if (k >= 1 && k <= N && (f || pt)) constrained = true;
+    }
+    if (!incr) {
+        const int C = ((N - 4) * (N - 3)) >> 1;
+        for (int k = tid; k < C; k += NT) L.qm[k] = INF16;
+    }
+    constrained = __syncthreads_or(constrained);
+    if (tid == 0) {
+        L.S[0] = L.S[N];
+        L.S[N + 1] = L.S[1];
+    }
+    const int mL = XS->motif_len;
+    if ((mh0 || mh1) && mL > 0) {
+        for (int o = tid + 1; o + mL - 1 <= N; o += NT) {
+            bool ok = true;
+            for (int k = 0; k < mL && ok; k++) ok = L.S[o + k] == mcode[k];
+            L.mat[o] = ok ? 1 : 0;
+        }
+        __syncthreads();
+        for (int o = 1 + wid; o + mL - 1 <= N; o += NT / WAVE) {
+            if (!uni(L.mat[o])) continue;
+            bool ok = true;
+            for (int k = lane; k < mL; k += WAVE) {
+                const int pk = mpt[k];
+                if (pk < 0) ok = ok && L.up[o + k] >= 1;
+                else if (pk > k) ok = ok && allowed(L, o + k, o + pk);
+            }
+            const bool all = __ballot(!ok) == 0;
+            if (lane == 0) L.mat[o] = all ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    const u32 mlclosing = __float_as_uint(XS->mlclosing);
+    const u32 mlbase = __float_as_uint(XS->mlbase_sig);
+    const u32 mx = __float_as_uint(XS->motif_extra);
+    const u32 mextra = (mh0 ? (mx & 0xFFFFu) : 0x7FFFu) | (mh1 ? (mx & 0xFFFF0000u) : 0x7FFF0000u);
+    const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
+    if (tid == 0) {
+        L.q5[0] = 0u;
+        for (int j = 1; j <= 4 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] : INF16;
+    }
+    // ---- per-cell setup (mfe_cells.hip): inner-pair code, hairpin (+ motif) or the
+    // non-pairable mark, multiloop stem of the pairable cells
+    for (int dd = 4 + wid; dd <= N - 1; dd += NWV) {
+        const int od = off(dd, N);
+        const int u = dd - 1;
+        const int lo = clo(dd), hi = chi(dd);
+        for (int r = lane; r < N - dd; r += WAVE) {
+            const int i = r + 1, j = i + dd;
+            const int si = L.S[i], sj = L.S[j], sim = L.S[i - 1], sjp = L.S[j + 1];
+            const int type = ptype(si, sj);
+            L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
+            if (i < lo || i > hi) continue;
+            const bool pr = type != 0 && allowed(L, i, j);
+            u32 h = INF16, m1 = INF16;
+            if (pr) {
+                if (L.up[i + 1] >= u) {
+                    bool special = false;
+                    if (u == 3 || u == 4 || u == 6) {
+                        const uint32_t key = hp_key(L.S, i, u + 2);
+                        for (int q0 = 0; q0 < nsp; q0 += 8) {
+#pragma unroll
+                            for (int t = 0; t < 8; t++)
+                                if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
+                        }
+                    }
+                    if (!special)
+                        h = padd(__float_as_uint(XS->hp[u]), (u == 3) ? L.dt[DT_TAU + type]
+                                                           : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
+                }
+                if (dd == mL - 1 && mL > 0 && L.mat[i]) h = pmin(h, mextra);
+                m1 = L.dt[DT_MLS + type * 25 + sim * 5 + sjp];
+            }
+            L.qbm[od + r] = pr ? h : MARK16;
+            L.qm1[colb(j) + i - 1] = m1;
+        }
+    }
+    __syncthreads();
+    // the partial, split and U slots start impossible (the setup used their space)
+    for (int k = tid; k < 4 * 2 * NP; k += NT) L.part[k] = PINF;
+    for (int k = tid; k < 6 * NP; k += NT) L.mla[k] = INF16;
+    for (int k = tid; k < 4 * NP; k += NT) L.colmin[k] = INF16;
+    __syncthreads();
+
+    const DevTables &T = *TT;
+    const u32 *T11 = reinterpret_cast<const u32 *>(&T.int11[0][0][0][0]);
+    const u32 *T21 = reinterpret_cast<const u32 *>(&T.int21[0][0][0][0][0]);
+    const u32 *T22 = reinterpret_cast<const u32 *>(&T.int22[0][0][0][0][0][0]);
+    const u32 tauE = gct[CT_FSM + 6];
+    const u32 fsm5 = gct[CT_FSM + 5];
+    const u32 fs1 = gct[CT_FSM + 1];
+    BUni U;
+    U.qbm = L.qbm;
+    U.cc = L.cc;
+    U.ct = L.ct;
+    U.gct = gct;
+    U.kg = reinterpret_cast<const uint4 *>(XS->ku16);
+    U.aq = lds_addr(L.qbm);
+    U.ac = lds_addr(L.cc);
+    U.act = lds_addr(L.ct);
+    U.fs1 = fs1;
+    U.il = reinterpret_cast<const u32 *>(XS->il);
+    U.nin = reinterpret_cast<const u32 *>(XS->nin);
+    U.N = N;
+    const uint32_t aqm = lds_addr(L.qm), aqm1 = lds_addr(L.qm1), ae4 = lds_addr(L.e4);
+    constexpr int L_WAVE = 4;           // the list of the next step's two diagonals and their B records
+    constexpr int Q_WAVE = 3;           // q5 of two columns
+    constexpr int fw[2] = {1, 5};       // finalize lane-sets 0, 1 (rows 1..64, 64..127)
+    int fls = -1;
+    for (int k = 0; k < 2; k++)
+        if (fw[k] == wid) fls = k;
+
+#ifdef ADX_STAMP
+    unsigned long long st_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+    st_acc[8] = st_last - st_setup0;
+#endif
+    const int NP2 = 2 * NP;
+    for (int d = 6; d - 3 <= N; d += 2) {
+        const int par = (d >> 1) & 1;
+        PSTAMP(0);
+        // ---------------- L: the pairable cells of diagonals d+2, d+3 (B's lanes next
+        // step; their qbm marks are the setup's) and the records of ranks < 64
+        if (wid == L_WAVE) {
+            __builtin_amdgcn_s_setprio(PRIO_ROLE);
+            const int pn = 1 - par;
+            int base = 0, P0 = 0;
+            for (int k = 0; k < 2; k++) {
+                const int dn = d + 2 + k;
+                if (k == 1) P0 = base;
+                if (dn > N - 1) continue;
+                const int lo = clo(dn), hi = chi(dn);
+                const int Ln = lanesets(hi - lo + 1);
+                for (int ls = 0; ls < Ln; ls++) {
+                    const int i = lo + ls * WAVE + lane;
+                    const bool pr = i <= hi && L.qbm[off(dn, N) + i - 1] != MARK16;
+                    const uint64_t m = __ballot(pr);
+                    const int rk = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                    if (pr) L.cl[pn * NP2 + rk] = uint8_t(i);
+                    if (pr && rk < WAVE) {
+                        const int j = i + dn;
+                        const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+                        const u32 mmo = L.dt[DT_MMI + oc];
+                        u32 *rr = L.rec + pn * 3 * WAVE + rk;
+                        rr[0] = uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) |
+                                (uint32_t(L.dn[j - 1]) << 24);
+                        rr[WAVE] = mmo;
+                        rr[2 * WAVE] = padd(L.ct[CT_ONEN + oc], mmo);
+                    }
+                    base += __popcll(m);
+                }
+            }
+            if (lane == 0) {
+                L.cnt[2 * pn] = P0;
+                L.cnt[2 * pn + 1] = base;
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        PSTAMP(1);
+        // ---------------- F: finalize e0 = d-2 and e1 = d-1.  Lanes = rows i (all
+        // rows: the unpaired part U is kept for every cell); a lane-set spans 64 rows,
+        // consecutive lane-sets overlap by one row (lane 63 recomputes the next set's
+        // first row for its U and writes nothing), so no value crosses waves.
+        {
+            const int e0 = d - 2, e1 = d - 1;
+            const int R = N - e0;                                   // rows of span e0 (e1: R - 1)
+            const int Lf = R <= 64 ? 1 : (R - 1 + 62) / 63;
+            if (e0 <= N - 1 && fls >= 0 && fls < Lf) {
+                __builtin_amdgcn_s_setprio(PRIO_ROLE);
+                const int i0 = 1 + fls * 63 + lane;
+                const bool own = lane < 63 || fls == Lf - 1;         // the overlap lane writes nothing
+                const bool rowA = i0 <= R, rowB = i0 <= R - 1;
+                const int i = rowA ? i0 : R;                         // every lane reads (batch)
+                const int jA = i + e0;
+                const int ceA = off(e0, N) + i - 1, ceB = off(e1, N) + i - 1;
+                const int cmA = colb(jA) + i - 1, cmB = colb(jA + 1) + i - 1;
+                // inner cells of the stack / bulge-1 shapes: spans e0-3, e0-2, e0-1
+                const int s3 = max(e0 - 3, 3), s2 = max(e0 - 2, 3), s1 = max(e0 - 1, 3);
+                const int c3 = off(s3, N) + i, c2 = off(s2, N) + i, c1 = off(s1, N) + i;
+                u32 initA, cceA, stA, pqA, mlA, spA, upA, a0, a1, vS3, cS3, vS3b, cS3b, vS2, cS2, vS2b, cS2b, vS1, cS1;
+                u32 initB, cceB, stB, mlB, spB, b0, b1;
+                uint32_t si, si1, sjm, sj, sjp, ui, ui1, ujA, ujB, djm, dj;
+                {
+                    const uint32_t aq = U.aq, ac = U.ac;
+                    const uint32_t pA = lds_addr(L.part) + uint32_t(((e0 & 3) * 2 * NP) + i) * 4u;
+                    const uint32_t pB = lds_addr(L.part) + uint32_t(((e1 & 3) * 2 * NP) + i) * 4u;
+                    const uint32_t mA = lds_addr(L.mla) + uint32_t(((e0 + 4) % 6) * NP + i + 1) * 4u;   // span e0-2
+                    const uint32_t mB = lds_addr(L.mla) + uint32_t(((e1 + 4) % 6) * NP + i + 1) * 4u;
+                    const uint32_t sA = lds_addr(L.mla) + uint32_t((e0 % 6) * NP + i) * 4u;
+                    const uint32_t sB = lds_addr(L.mla) + uint32_t((e1 % 6) * NP + i) * 4u;
+                    const uint32_t uA = lds_addr(L.colmin) + uint32_t(((e0 + 3) & 3) * NP + jA) * 4u;  // span e0-1
+                    const uint32_t aS = lds_addr(L.S), aU = lds_addr(L.up), aD = lds_addr(L.dn);
+                    asm volatile(
+                        "ds_read_b32 %[initA], %[qA]\n"
+                        "ds_read_u8 %[cceA], %[kA]\n"
+                        "ds_read_b32 %[stA], %[q1A]\n"
+                        "ds_read_b32 %[pqA], %[q1P]\n"
+                        "ds_read_b32 %[mlA], %[mA]\n"
+                        "ds_read_b32 %[spA], %[sA]\n"
+                        "ds_read_b32 %[upA], %[uA]\n"
+                        "ds_read_b32 %[a0], %[pA]\n"
+                        "ds_read_b32 %[a1], %[pA] offset:%[pst]\n"
+                        "ds_read_b32 %[initB], %[qB]\n"
+                        "ds_read_u8 %[cceB], %[kB]\n"
+                        "ds_read_b32 %[stB], %[q1B]\n"
+                        "ds_read_b32 %[mlB], %[mB]\n"
+                        "ds_read_b32 %[spB], %[sB]\n"
+                        "ds_read_b32 %[b0], %[pB]\n"
+                        "ds_read_b32 %[b1], %[pB] offset:%[pst]\n"
+                        "ds_read_b32 %[vS3], %[q3]\n"
+                        "ds_read_b32 %[vS3b], %[q3] offset:4\n"
+                        "ds_read_b32 %[vS2], %[q2]\n"
+                        "ds_read_b32 %[vS2b], %[q2] offset:4\n"
+                        "ds_read_b32 %[vS1], %[q1]\n"
+                        "ds_read_u8 %[cS3], %[k3]\n"
+                        "ds_read_u8 %[cS3b], %[k3] offset:1\n"
+                        "ds_read_u8 %[cS2], %[k2]\n"
+                        "ds_read_u8 %[cS2b], %[k2] offset:1\n"
+                        "ds_read_u8 %[cS1], %[k1]\n"
+                        "ds_read_u8 %[si], %[aSi]\n"
+                        "ds_read_u8 %[si1], %[aSi] offset:1\n"
+                        "ds_read_u8 %[sjm], %[aSj] offset:0\n"
+                        "ds_read_u8 %[sj], %[aSj] offset:1\n"
+                        "ds_read_u8 %[sjp], %[aSj] offset:2\n"
+                        "ds_read_u8 %[ui], %[aUi]\n"
+                        "ds_read_u8 %[ui1], %[aUi] offset:1\n"
+                        "ds_read_u8 %[ujA], %[aUj]\n"
+                        "ds_read_u8 %[ujB], %[aUj] offset:1\n"
+                        "ds_read_u8 %[djm], %[aDj] offset:0\n"
+                        "ds_read_u8 %[dj], %[aDj] offset:1\n"
+                        "s_waitcnt lgkmcnt(0)"
+                        : [initA] "=&v"(initA), [cceA] "=&v"(cceA), [stA] "=&v"(stA), [pqA] "=&v"(pqA), [mlA] "=&v"(mlA),
+                          [spA] "=&v"(spA), [upA] "=&v"(upA), [a0] "=&v"(a0), [a1] "=&v"(a1), [initB] "=&v"(initB),
+                          [cceB] "=&v"(cceB), [stB] "=&v"(stB), [mlB] "=&v"(mlB), [spB] "=&v"(spB), [b0] "=&v"(b0),
+                          [b1] "=&v"(b1), [vS3] "=&v"(vS3), [vS3b] "=&v"(vS3b), [vS2] "=&v"(vS2), [vS2b] "=&v"(vS2b),
+                          [vS1] "=&v"(vS1), [cS3] "=&v"(cS3), [cS3b] "=&v"(cS3b), [cS2] "=&v"(cS2), [cS2b] "=&v"(cS2b),
+                          [cS1] "=&v"(cS1), [si] "=&v"(si), [si1] "=&v"(si1), [sjm] "=&v"(sjm), [sj] "=&v"(sj),
+                          [sjp] "=&v"(sjp), [ui] "=&v"(ui), [ui1] "=&v"(ui1), [ujA] "=&v"(ujA), [ujB] "=&v"(ujB),
+                          [djm] "=&v"(djm), [dj] "=&v"(dj)
+                        : [qA] "v"(aq + uint32_t(ceA) * 4u), [kA] "v"(ac + uint32_t(ceA)),
+                          [q1A] "v"(aqm1 + uint32_t(cmA) * 4u), [q1P] "v"(aqm1 + uint32_t(colb(jA - 1) + i - 1) * 4u),
+                          [mA] "v"(mA), [sA] "v"(sA), [uA] "v"(uA), [pA] "v"(pA), [pst] "i"(NM * 4 + 8),
+                          [qB] "v"(aq + uint32_t(ceB) * 4u), [kB] "v"(ac + uint32_t(ceB)),
+                          [q1B] "v"(aqm1 + uint32_t(cmB) * 4u), [mB] "v"(mB), [sB] "v"(sB), [pB] "v"(pB),
+                          [q3] "v"(aq + uint32_t(c3) * 4u), [q2] "v"(aq + uint32_t(c2) * 4u), [q1] "v"(aq + uint32_t(c1) * 4u),
+                          [k3] "v"(ac + uint32_t(c3)), [k2] "v"(ac + uint32_t(c2)), [k1] "v"(ac + uint32_t(c1)),
+                          [aSi] "v"(aS + uint32_t(i)), [aSj] "v"(aS + uint32_t(jA - 1)), [aUi] "v"(aU + uint32_t(i)),
+                          [aUj] "v"(aU + uint32_t(jA)), [aDj] "v"(aD + uint32_t(jA - 1))
+                        : "memory");
+                }
+                static_assert(NM + 2 == PLay<NM>::NP, "partial halves are NP words apart");
+                // the loop-correction factors of the stack / bulge-1 shapes and the cells' own terms
+                const int tyA = ptype(si, sj), tyB = ptype(si, sjp);
+                const int t8A = tyA * 8, t8B = tyB * 8;
+                auto stk = [&](u32 v, u32 c, int t8) {   // inner pair with code c closing a stack with type t8/8
+                    return padd(v, padd(L.ct[CT_INVMM + c], L.ct[CT_STK + t8 + ((int(c) * 41) >> 10)]));
+                };
+                // A = (i, jA): stack inner (i+1, jA-1) span e0-2 [vS2]; bulges (0,1) inner
+                // (i+1, jA-2) [vS3], (1,0) inner (i+2, jA-1) [vS3b], span e0-3.
+                // B = (i, jA+1): stack inner (i+1, jA) span e0-1 [vS1]; bulges (0,1) inner
+                // (i+1, jA-1) [vS2], (1,0) inner (i+2, jA) [vS2b], span e0-2.
+                u32 iA = INF16, iB = INF16;
+                if (e0 >= 6) iA = stk(vS2, cS2, t8A);
+                if (e0 >= 7) {
+                    iA = pmin(iA, djm >= 1 ? padd(stk(vS3, cS3, t8A), fs1) : INF16);
+                    iA = pmin(iA, ui1 >= 1 ? padd(stk(vS3b, cS3b, t8A), fs1) : INF16);
+                }
+                if (e1 >= 6) iB = stk(vS1, cS1, t8B);
+                if (e1 >= 7) {
+                    iB = pmin(iB, dj >= 1 ? padd(stk(vS2, cS2, t8B), fs1) : INF16);
+                    iB = pmin(iB, ui1 >= 1 ? padd(stk(vS2b, cS2b, t8B), fs1) : INF16);
+                }
+                const u32 mlclA = padd(mlclosing, L.dt[DT_MLS + rtype(tyA) * 25 + sjm * 5 + si1]);
+                const u32 mlclB = padd(mlclosing, L.dt[DT_MLS + rtype(tyB) * 25 + sj * 5 + si1]);
+                const u32 mmiA = L.dt[DT_MMI + cceA], mmiB = L.dt[DT_MMI + cceB];
+                const bool inA = rowA && (!incr || (i >= clo(e0) && i <= chi(e0)));
+                const bool inB = rowB && e1 <= N - 1 && (!incr || (i >= clo(e1) && i <= chi(e1)));
+                // cell A
+                u32 q1A = stA;   // restored qm1 outside the band
+                if (inA) {
+                    const u32 prev = (e0 >= 5 && ujA >= 1) ? padd(pqA, mlbase) : INF16;
+                    u32 f1 = prev;
+                    if (initA != MARK16) {
+                        u32 c = pmin(initA, pack2(int(a0), int(a1)));
+                        c = pmin(c, iA);
+                        c = pfin(pmin(c, padd(mlA, mlclA)));
+                        if (own) L.qbm[ceA] = pfin(padd(c, mmiA));
+                        f1 = pmin(padd(c, stA), prev);
+                    }
+                    q1A = pfin(f1);
+                    if (own) L.qm1[cmA] = q1A;
+                }
+                const u32 UA = ui >= 1 ? pmin(q1A, padd(upA, mlbase)) : q1A;
+                // cell B (its qm1 predecessor (i, jA) is cell A of this lane)
+                u32 q1B = stB;
+                if (inB) {
+                    const u32 prev = (e1 >= 5 && ujB >= 1) ? padd(q1A, mlbase) : INF16;
+                    u32 f1 = prev;
+                    if (initB != MARK16) {
+                        u32 c = pmin(initB, pack2(int(b0), int(b1)));
+                        c = pmin(c, iB);
+                        c = pfin(pmin(c, padd(mlB, mlclB)));
+                        if (own) L.qbm[ceB] = pfin(padd(c, mmiB));
+                        f1 = pmin(padd(c, stB), prev);
+                    }
+                    q1B = pfin(f1);
+                    if (own) L.qm1[cmB] = q1B;
+                }
+                // U of row i+1 in column jA+1 (span e0) is the next lane's cell A
+                const u32 UA1 = u32(__builtin_amdgcn_ds_bpermute((lane + 1) * 4, int(UA)));
+                const u32 UB = ui >= 1 ? pmin(q1B, padd(UA1, mlbase)) : q1B;
+                if (own && rowA) {
+                    L.colmin[(e0 & 3) * NP + jA] = UA;
+                    L.part[(e0 & 3) * 2 * NP + i] = PINF;
+                    L.part[(e0 & 3) * 2 * NP + NP + i] = PINF;
+                    if (e0 <= N - 3 && (!incr || (i >= qlo(e0) && i <= qhi(e0))))
+                        L.qm[rowb(i, N) + e0 - 4] = pfin(pmin(e0 >= 9 ? spA : INF16, UA));
+                }
+                if (own && rowB && e1 <= N - 1) {
+                    L.colmin[(e1 & 3) * NP + jA + 1] = UB;
+                    L.part[(e1 & 3) * 2 * NP + i] = PINF;
+                    L.part[(e1 & 3) * 2 * NP + NP + i] = PINF;
+                    if (e1 <= N - 3 && (!incr || (i >= qlo(e1) && i <= qhi(e1))))
+                        L.qm[rowb(i, N) + e1 - 4] = pfin(pmin(e1 >= 9 ? spB : INF16, UB));
+                }
+                __builtin_amdgcn_s_setprio(0);
+            }
+        }
+        PSTAMP(2);
+        // ---------------- B: interior-loop partials (u >= 2) of diagonals d and d+1.
+        // Lanes = the pairable cells of both (listed last step: ranks < P0 on d,
+        // the rest on d+1); a lane of d+1 reads its inner cells at
+        // off(d - 2 - u) + i + (N - d + 2 + u), which the blocks add per lane (hb).
+        if (d + 1 >= 8 && d <= N - 1) {
+            const int P0 = L.cnt[2 * par], P = L.cnt[2 * par + 1];
+            const int sh = P <= 16 ? 2 : (P <= 32 ? 1 : 0);   // log2 slices per cell
+            const int cwl = 6 - sh;
+            const int Lb = (P + (1 << cwl) - 1) >> cwl;
+            const int blk = wid;
+            const int r = lane >> cwl;
+            U.d = d;
+            U.umax = d - 5 < 30 ? d - 5 : 30;   // d+1's loop sizes; d's last one reads the impossible span 3
+            for (int ls = 0; ls < Lb && blk < MFE_NBLK; ls++) {
+                const int idx = (ls << cwl) + (lane & ((1 << cwl) - 1));
+                if (idx < P) {
+                    const int hb = idx >= P0 ? 1 : 0;
+                    const int dd = d + hb;
+                    int i, oc, cA, cB;
+                    u32 mmo, mo;
+                    if (idx < WAVE) {
+                        const u32 *rr = L.rec + par * 3 * WAVE + idx;
+                        const u32 wd = rr[0];
+                        mmo = rr[WAVE];
+                        mo = rr[2 * WAVE];
+                        i = wd & 255;
+                        oc = (wd >> 8) & 255;
+                        cA = (wd >> 16) & 255;
+                        cB = wd >> 24;
+                    } else {
+                        i = L.cl[par * NP2 + idx];
+                        oc = ptype(L.S[i], L.S[i + dd]) * 25 + L.S[i + 1] * 5 + L.S[i + dd - 1];
+                        cA = L.up[i + 1];
+                        cB = L.dn[i + dd - 1];
+                        mmo = L.dt[DT_MMI + oc];
+                        mo = padd(L.ct[CT_ONEN + oc], mmo);
+                    }
+                    const int type = (oc * 41) >> 10;
+                    const int si1 = (oc / 5) % 5;
+                    const int sj1 = oc % 5;
+                    const int uml = dd - 6 < 30 ? dd - 6 : 30;   // this lane's loop sizes
+                    BCell C;
+                    C.i = i + hb * (N - d + 2);
+                    C.hb = hb;
+                    C.ty8 = type * 8;
+                    C.rs = uint32_t(r) * 4u;
+                    C.ee = ae4 + uint32_t(r) * 4u;
+                    C.r1 = (r & 1) != 0;
+                    C.r2 = (r & 2) != 0;
+                    C.eb = r & 1;
+                    C.ea = sh == 2 ? ((r & 1) ? -(r >> 1) : (r >> 1)) : ((r & 1) ? -1 : 1);
+                    C.ctb = (r & 2) ? CT_ONEN : CT_BUL;
+                    C.A = cA;
+                    C.B = cB;
+                    const u32 tau = type > 2 ? tauE : 0u;
+                    C.m23f = padd(L.ct[CT_M23O + oc], fsm5);
+                    C.t11 = C.t12 = C.t21 = C.t22 = INF16;
+                    const unsigned tbm = sh == 2 ? MFE_TABLE_BLOCKS_S4 : sh == 1 ? MFE_TABLE_BLOCKS_S2 : MFE_TABLE_BLOCKS;
+                    if ((tbm >> blk) & 1) {   // 1x1..2x2 energies from HBM (L2), used at the block end
+                        const int ty8 = type * 8;
+                        if (uml >= 2) {
+                            const int c2 = L.cc[off(dd - 4, N) + i + 1];
+                            C.t11 = T11[((ty8 + ((c2 * 41) >> 10)) * 5 + si1) * 5 + sj1];
+                        }
+                        if (uml >= 3) {
+                            const int o3 = off(dd - 5, N) + i;
+                            const int a2 = L.cc[o3 + 1], b2 = L.cc[o3 + 2];
+                            const int ta = (a2 * 41) >> 10, tb = (b2 * 41) >> 10;
+                            C.t12 = T21[(((ty8 + ta) * 5 + si1) * 5 + (a2 / 5) % 5) * 5 + sj1];
+                            C.t21 = T21[(((tb * 8 + type) * 5 + (b2 / 5) % 5) * 5 + si1) * 5 + b2 % 5];
+                        }
+                        if (uml >= 4) {
+                            const int c2 = L.cc[off(dd - 6, N) + i + 2];
+                            const int t2 = (c2 * 41) >> 10;
+                            C.t22 = T22[((((ty8 + t2) * 5 + si1) * 5 + c2 % 5) * 5 + (c2 / 5) % 5) * 5 + sj1];
+                        }
+                    }
+                    Acc a{INF16, INF16, INF16, INF16, INF16, INF16};
+                    const bool mk = constrained && __ballot(C.A < uml || C.B < uml) != 0;
+                    U.mk = mk;
+                    PSTAMP(9);
+                    if (sh == 2) mfe_block_s4(blk, U, C, a);
+                    else if (sh == 1) mfe_block_s2(blk, U, C, a);
+                    else mfe_block(blk, U, C, a);
+                    PSTAMP(10);
+                    u32 acc = pmin(pmin(a.s, padd(pmin(a.g0, a.g1), mmo)), pmin(padd(a.b, tau), padd(a.n, mo)));
+                    if (sh == 2) acc = pmin(acc, padd(a.e, C.r2 ? mo : tau));
+                    if (sh == 2) acc = fold_rows16(acc);
+                    if (sh >= 1) acc = fold_halves(acc);
+                    if (r == 0) {
+                        int *pp = L.part + (dd & 3) * 2 * NP + i;
+                        atomicMin(pp, sext_lo(acc));
+                        atomicMin(pp + NP, sext_hi(acc));
+                    }
+                }
+            }
+        }
+        PSTAMP(3);
+        // ---------------- M: split parts of qm for spans d and d+1 (lanes = cells x
+        // slices of the split points, mfe_cells.hip): min over t >= 5 of
+        // qm(i, i+t-1) + qm1(i+t, j), written to the span's slot for F
+        if (wid == MA_WAVE) {
+            __builtin_amdgcn_s_setprio(PRIO_ROLE);
+            for (int s = d; s <= d + 1; s++) {
+                if (s < 9 || s > N - 3) continue;   // no split point below span 9
+                const int lo = qlo(s), hi = qhi(s);
+                const int Lm = lanesets(hi - lo + 1);
+                const int Tt = s - 4;
+                u32 *slot = L.mla + (s % 6) * NP;
+                for (int ls = 0; ls < Lm; ls++) {
+                    const int nc = min(WAVE, hi - lo + 1 - ls * WAVE);
+                    const int lc = nc <= 1 ? 0 : 32 - __clz(nc - 1);
+                    const int cst = 1 << lc, lsl = 6 - lc;
+                    const int c = lane & (cst - 1), rr = lane >> lc;
+                    int i = lo + ls * WAVE + c;
+                    const bool valid = c < nc;
+                    if (!valid) i = hi;
+                    const int j = i + s;
+                    const int nb = Tt - 4;                                  // split points t = 5..Tt
+                    const int bs = nb > 0 ? (nb + (1 << lsl) - 1) >> lsl : 0;
+                    const int ta = 5 + rr * bs;
+                    u32 sp0 = INF16, sp1 = INF16;
+                    const int nch = (bs + 15) >> 4;
+                    for (int ch = 0; ch < nch; ch++) {
+                        const int t0 = ta + ch * 16;
+                        u32 av[16], rv[16];
+                        {
+                            const uint32_t pa = aqm1 + uint32_t(colb(j) + i - 1 + t0) * 4u;
+                            const uint32_t pr = aqm + uint32_t(rowb(i, N) - 5 + t0) * 4u;
+                            asm volatile(
+                                    "ds_read_b32 %0, %32 offset:0\n"
+                                    "ds_read_b32 %1, %32 offset:4\n"
+                                    "ds_read_b32 %2, %32 offset:8\n"
+                                    "ds_read_b32 %3, %32 offset:12\n"
+                                    "ds_read_b32 %4, %32 offset:16\n"
+                                    "ds_read_b32 %5, %32 offset:20\n"
+                                    "ds_read_b32 %6, %32 offset:24\n"
+                                    "ds_read_b32 %7, %32 offset:28\n"
+                                    "ds_read_b32 %8, %32 offset:32\n"
+                                    "ds_read_b32 %9, %32 offset:36\n"
+                                    "ds_read_b32 %10, %32 offset:40\n"
+                                    "ds_read_b32 %11, %32 offset:44\n"
+                                    "ds_read_b32 %12, %32 offset:48\n"
+                                    "ds_read_b32 %13, %32 offset:52\n"
+                                    "ds_read_b32 %14, %32 offset:56\n"
+                                    "ds_read_b32 %15, %32 offset:60\n"
+                                    "ds_read_b32 %16, %33 offset:0\n"
+                                    "ds_read_b32 %17, %33 offset:4\n"
+                                    "ds_read_b32 %18, %33 offset:8\n"
+                                    "ds_read_b32 %19, %33 offset:12\n"
+                                    "ds_read_b32 %20, %33 offset:16\n"
+                                    "ds_read_b32 %21, %33 offset:20\n"
+                                    "ds_read_b32 %22, %33 offset:24\n"
+                                    "ds_read_b32 %23, %33 offset:28\n"
+                                    "ds_read_b32 %24, %33 offset:32\n"
+                                    "ds_read_b32 %25, %33 offset:36\n"
+                                    "ds_read_b32 %26, %33 offset:40\n"
+                                    "ds_read_b32 %27, %33 offset:44\n"
+                                    "ds_read_b32 %28, %33 offset:48\n"
+                                    "ds_read_b32 %29, %33 offset:52\n"
+                                    "ds_read_b32 %30, %33 offset:56\n"
+                                    "ds_read_b32 %31, %33 offset:60\n"
+                                "s_waitcnt lgkmcnt(0)"
+                                : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(av[6]), "=&v"(av[7]), "=&v"(av[8]), "=&v"(av[9]), "=&v"(av[10]), "=&v"(av[11]), "=&v"(av[12]), "=&v"(av[13]), "=&v"(av[14]), "=&v"(av[15]), "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3]), "=&v"(rv[4]), "=&v"(rv[5]), "=&v"(rv[6]), "=&v"(rv[7]), "=&v"(rv[8]), "=&v"(rv[9]), "=&v"(rv[10]), "=&v"(rv[11]), "=&v"(rv[12]), "=&v"(rv[13]), "=&v"(rv[14]), "=&v"(rv[15])
+                                : "v"(pa), "v"(pr)
+                                : "memory");
+                        }
+                        // reads past this slice's end belong to the next slice (a split point
+                        // counted twice leaves the minimum unchanged): only the row end Tt masks
+                        const int lim = Tt - t0;
+                        if (__ballot(lim < 15) == 0) {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                sp0 = pmin(sp0, padd(rv[k], av[k]));
+                                sp1 = pmin(sp1, padd(rv[k + 1], av[k + 1]));
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 16; k += 2) {
+                                sp0 = pmin(sp0, padd(rv[k], k <= lim ? av[k] : INF16));
+                                sp1 = pmin(sp1, padd(rv[k + 1], k + 1 <= lim ? av[k + 1] : INF16));
+                            }
+                        }
+                    }
+                    u32 split = pmin(sp0, sp1);
+                    for (int k = cst; k < WAVE; k <<= 1) split = pmin(split, u32(__shfl_xor(int(split), k, WAVE)));
+                    if (valid && rr == 0) slot[i] = pfin(split);
+                }
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        PSTAMP(4);
+        // ---------------- Q: q5[j] for j = d-3, d-2 (qbm spans <= d-3 are final)
+        if (wid == Q_WAVE) {
+            const int j0 = d - 3, j1 = d - 2;
+            const bool w0 = j0 >= 5 && j0 <= N && (!incr || j0 >= m_lo - 1);
+            const bool w1 = j1 >= 5 && j1 <= N && (!incr || j1 >= m_lo - 1);
+            if (w0 || w1) {
+                __builtin_amdgcn_s_setprio(PRIO_ROLE);
+                const int s0 = L.S[j0], s1 = L.S[j1];
+                const int sp0 = L.S[j0 + 1], sp1 = (j1 < N) ? L.S[j1 + 1] : 5;   // j0 < N whenever j1 <= N
+                u32 acc0 = INF16, acc1 = INF16;
+                for (int k0 = 1; k0 <= j1 - 4; k0 += WAVE) {
+                    const int kk = k0 + lane;
+                    const bool ok1 = kk <= j1 - 4, ok0 = kk <= j0 - 4;
+                    const int k = ok1 ? kk : 1;
+                    const int sk = L.S[k], skm = (k > 1) ? L.S[k - 1] : 5;
+                    const u32 q5k = L.q5[k - 1];
+                    const int ix1 = off(j1 - k, N) + k - 1;
+                    const int ix0 = off(max(j0 - k, 4), N) + k - 1;
+                    const u32 ex1 = L.dt[DT_EXT + ptype(sk, s1) * 36 + skm * 6 + sp1];
+                    const u32 ex0 = L.dt[DT_EXT + ptype(sk, s0) * 36 + skm * 6 + sp0];
+                    const u32 t1 = padd(padd(q5k, L.qbm[ix1]), padd(L.ct[CT_INVMM + L.cc[ix1]], ex1));
+                    const u32 t0 = padd(padd(q5k, L.qbm[ix0]), padd(L.ct[CT_INVMM + L.cc[ix0]], ex0));
+                    acc1 = pmin(acc1, ok1 ? t1 : INF16);
+                    acc0 = pmin(acc0, ok0 ? t0 : INF16);
+                }
+                const u32 red0 = wave_min(acc0), red1 = wave_min(acc1);
+                if (lane == 0) {
+                    u32 q0 = L.q5[j0];   // restored (refold) or initial when not recomputed
+                    if (w0) {
+                        q0 = pfin(pmin((L.up[j0] >= 1) ? L.q5[j0 - 1] : INF16, red0));
+                        L.q5[j0] = q0;
+                    }
+                    if (w1) L.q5[j1] = pfin(pmin((L.up[j1] >= 1) ? q0 : INF16, red1));
+                }
+                __builtin_amdgcn_s_setprio(0);
+            }
+        }
+        PSTAMP(5);
+        lds_barrier();
+        PSTAMP(6);
+    }
+#ifdef ADX_STAMP
+    if (lane == 0 && wid < 16)
+        for (int k = 0; k < 15; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
+#endif
+    z = L.q5[N];
+    if (inc.dst) {   // this fold's tables: the next proposal's unchanged cells
+        const size_t C = size_t(ka.cells);
+        u32 *dp = inc.dst;
+        for (int k = tid; k < int(C); k += NT) {
+            dp[k] = L.qbm[k];
+            dp[C + k] = L.qm[k];
+            dp[2 * C + k] = L.qm1[k];
+        }
+        for (int k = tid; k <= N; k += NT) dp[3 * C + k] = L.q5[k];
+    }
+    bool low = false;
+    const int C = ((N - 4) * (N - 3)) >> 1;
+    auto chk = [&](u32 x) {
+        const s16x2 q = sv(x);
+        low |= (q.x < MFE16_FLOOR) || (q.y < MFE16_FLOOR);
+    };
+    for (int k = tid; k < C; k += NT) {
+        chk(L.qbm[k]);
+        chk(L.qm[k]);
+        chk(L.qm1[k]);
+    }
+    for (int k = tid; k <= N; k += NT) chk(L.q5[k]);
+    bad = __syncthreads_or(low);
+}
+
+constexpr int MFE_WPE = (2 * NWV + 3) / 4;
+template <int NT, int NM>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFE_WPE, MFE_WPE)))
+mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTables *__restrict__ TT, const uint8_t *seqs,
+                int W, float *gout, const int *mask) {
+    // one workgroup per (walker, fold group), as mfe_cells_kernel
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const CP L = PLay<NM>::carve(smem);
+    const int ng = ka.n_groups2;
+    const int wb = int(blockIdx.x) / ng, g = int(blockIdx.x) % ng;
+    if (wb >= W) return;
+    const int w = ka.order ? ka.order[wb] : wb;
+    if (mask && mask[w] != 1) return;
+    {
+        const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
+        for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = gct[k];
+        const DevTables &T = *TT;
+        auto bits = [](float f) { return __float_as_uint(f); };
+        for (int k = threadIdx.x; k < 200; k += NT) {
+            L.dt[DT_MMH + k] = bits((&T.mmH[0][0][0])[k]);
+            L.dt[DT_MMI + k] = bits((&T.mmI[0][0][0])[k]);
+            L.dt[DT_MLS + k] = bits((&T.mlstem[0][0][0])[k]);
+        }
+        for (int k = threadIdx.x; k < 288; k += NT) L.dt[DT_EXT + k] = bits((&T.ext[0][0][0])[k]);
+        for (int k = threadIdx.x; k < 8; k += NT) L.dt[DT_TAU + k] = bits(T.termAU[k]);
+        for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
+        for (int k = threadIdx.x; k < MFE_E4_SLOTS * 4; k += NT) {
+            const int a = MFE_E4_A[k >> 2][k & 3];
+            L.e4[k] = a < 0 ? INF16 : XS->ku16[MFE_E4_U[k >> 2]][a];
+        }
+    }
+    __syncthreads();
+    const int vs[2] = {ka.groups2[2 * g], ka.groups2[2 * g + 1]};
+    IncM inc{nullptr, nullptr, 0, 0};
+    if (ka.tab) {
+        const size_t Gf = inc_group_floats(ka.cells, ka.Nmax, 1);
+        const int cur = ka.cur_slot[w];
+        float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
+        inc.dst = reinterpret_cast<u32 *>(base + size_t(1 - cur) * ka.tab_slot + size_t(g) * Gf);
+        // a sibling group may clear tab_valid[w] on overflow while this one reads it:
+        // either value is correct (an incremental refold equals a fold from scratch)
+        if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+            const int lb = ka.variants[vs[0]].before_len;
+            inc.src = reinterpret_cast<const u32 *>(base + size_t(cur) * ka.tab_slot + size_t(g) * Gf);
+            inc.m_lo = ka.chg[2 * w] + 1 + lb;
+            inc.m_hi = ka.chg[2 * w + 1] + 1 + lb;
+        }
+    }
+    u32 z = INF16;
+    bool bad = false;
+    mfe_pair_fold<NT, NM>(ka, XS, TT, vs, L.raw, L, z, bad, inc);
+    if (threadIdx.x == 0) {
+        const s16x2 q = sv(z);
+        const int hv[2] = {q.x, q.y};
+        for (int h = 0; h < 2; h++) {
+            const double e = hv[h] >= 0x4000 ? double(INFINITY) : static_cast<double>(hv[h]) / 100.0;
+            gout[size_t(w) * ka.n_variants + vs[h]] = static_cast<float>(e);
+        }
+        if (bad && ka.ovf) {
+            ka.ovf[w] = 1;
+            if (ka.tab) ka.tab_valid[w] = 0;
+        }
+    }
+}
+
+template <int NM>
+static hipError_t launch_pair_nm(const KArgs &ka, const uint8_t *seqs, int W, float *gout, const int *mask,
+                                 hipStream_t stream) {
+    constexpr size_t lds = PLay<NM>::BYTES;
+    auto k = mfe_pair_kernel<NWV * WAVE, NM>;
+    static bool configured = false;
+    if (!configured) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (e != hipSuccess) return e;
+        configured = true;
+    }
+    hipLaunchKernelGGL(k, dim3(W * ka.n_groups2), dim3(NWV * WAVE), lds, stream, ka, ka.X, ka.T, seqs, W, gout, mask);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// The pair kernel covers folded lengths up to 100 (two 100-nt walkers per CU).
+bool mfe_pair_covers(const KArgs &ka) { return ka.Nmax <= 100; }
+
+hipError_t launch_mfe_pair(const KArgs &ka, const uint8_t *seqs, int W, float *gout, const int *mask,
+                           hipStream_t stream) {
+    static_assert(PLay<100>::BYTES + 256 <= 80 * 1024, "two 100-nt walkers per CU");
+    if (ka.Nmax <= 64) return launch_pair_nm<64>(ka, seqs, W, gout, mask, stream);
+    if (ka.Nmax <= 100) return launch_pair_nm<100>(ka, seqs, W, gout, mask, stream);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace adx
+
+#ifdef ADX_STAMP
+extern "C" int adx_debug_stamps_pair(unsigned long long *out, int reset) {  // [16][16]
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_p), sizeof(adx::g_stamps_p)) != hipSuccess) return 1;
+    if (reset) {
+        static unsigned long long z[16][16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_p), z, sizeof(z)) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif

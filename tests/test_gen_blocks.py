@@ -80,5 +80,20 @@ def test_committed_blocks_match_generator(tmp_path):
     env = dict(os.environ, ADX_GEN_OUT=str(tmp_path))
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_mfe_blocks.py")], env=env,
                           stderr=subprocess.DEVNULL)
-    name = "mfe_blocks.inc"
-    assert filecmp.cmp(str(tmp_path / name), os.path.join(ROOT, "addapt_amd", "csrc", name), shallow=False), name
+    for name in ("mfe_blocks.inc", "mfe_pair_blocks.inc"):
+        assert filecmp.cmp(str(tmp_path / name), os.path.join(ROOT, "addapt_amd", "csrc", name), shallow=False), name
+
+
+def test_pair_partitions_skip_stack_and_bulge1():
+    """The pair kernel's blocks hold loop sizes 2..30 once each (the stack and
+    bulge-1 shapes run in its finalize, mfe_pair.hip) and add the per-lane
+    diagonal offset hb * u to every inner-cell address."""
+    G.PAIR = True
+    try:
+        for S in (1, 2, 4):
+            blocks, load = G.partition(S)
+            assert sorted(u for b in blocks for u in b) == list(range(2, G.MAXLOOP + 1)), S
+        pre = G.sliced_parts(17, 4, "a")[0]
+        assert "off(dd - 19, U.N) + ci + hb * 17" in pre[0]
+    finally:
+        G.PAIR = False

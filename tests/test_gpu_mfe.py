@@ -348,9 +348,12 @@ def workloads_par():
                         "addapt_amd", "data", "rna_turner2004_addapt.par")
 
 
-def test_fold_mfe_nonzero_mlbase(native, oracle, tmp_path):
+@pytest.mark.parametrize("pair", ["1", "0"])
+def test_fold_mfe_nonzero_mlbase(native, oracle, tmp_path, monkeypatch, pair):
     """A parameter set with MLbase != 0 folds through the direct unpaired-run
-    loop of the qm rows (not the column minima) and stays bit-exact."""
+    loop of the qm rows (not the column minima; the pair kernel's U recursion
+    adds MLbase per row) and stays bit-exact."""
+    monkeypatch.setenv("ADX_MFE_PAIR", pair)
     path = _par_with_mlbase(tmp_path, 30)
     P, OP = native.Params(path), oracle.Params(path)
     rng = random.Random(23)
@@ -369,13 +372,16 @@ def test_fold_mfe_nonzero_mlbase(native, oracle, tmp_path):
     assert oracle.mfe_energy(s, params=OP) >= oracle.mfe_energy(s)
 
 
-@pytest.mark.parametrize("kernel", ["rows", "cells"])
+@pytest.mark.parametrize("kernel", ["rows", "cells", "cells-single"])
 def test_mfe_kernels_score_and_trajectory(native, oracle, monkeypatch, kernel):
     """The general MFE kernel (score_kernel<MinPlus16>, lanes = terms: energy
-    models or lengths the cells kernel does not cover) and the default cells
-    kernel, selected per launch by ADX_MFE_KERNEL: scored folds bit-exact and an
-    incremental trajectory identical to the oracle's."""
-    monkeypatch.setenv("ADX_MFE_KERNEL", kernel)
+    models or lengths the cells kernel does not cover), the default cells
+    kernel (two diagonals per barrier, mfe_pair.hip, up to 100 nt) and the
+    one-diagonal cells kernel (ADX_MFE_PAIR=0, mfe_cells.hip), selected per
+    launch: scored folds bit-exact and an incremental trajectory identical to
+    the oracle's."""
+    monkeypatch.setenv("ADX_MFE_KERNEL", kernel.split("-")[0])
+    monkeypatch.setenv("ADX_MFE_PAIR", "0" if kernel == "cells-single" else "1")
     tmpl, active = workloads.synthetic(100)
     terms = workloads.default_objective()
     eng = _engine(native, tmpl, [active], terms,
@@ -444,3 +450,57 @@ def test_mc_trajectory_mfe_auto_zero_median(native, oracle):
         assert _close(scores[w], ref["score"])
         assert list(counters[w]) == ref["counters"]
     assert neg_zero > 0
+
+
+@pytest.mark.parametrize("N", [20, 27, 33, 48, 64, 65, 71, 99, 100])
+def test_pair_kernel_equals_single_and_oracle(native, oracle, monkeypatch, N):
+    """Two diagonals per barrier (mfe_pair.hip) against the one-diagonal kernel
+    and the oracle: random sequences (GC-rich ones too: every cell pairable,
+    lane-sets past 64 cells) under random hard constraints, both parities of N,
+    apo / holo, bit for bit."""
+    rng = random.Random(1000 + N)
+    seqs, csts = [], []
+    for k in range(12):
+        s = "".join(rng.choice("GC" if k % 4 == 3 else "ACGU") for _ in range(N))
+        seqs.append(s)
+        csts.append(rand_constraint(rng, N) if k % 2 else "." * N)
+    apt = (workloads.THEO_SEQ, workloads.THEO_FOLD, native.theo_energy())
+    motif = oracle.make_motif(workloads.THEO_SEQ, workloads.THEO_FOLD, oracle.theo_bonus())
+    terms = [("apo", 0, False, 1.0), ("holo", 0, True, 1.0)]
+    got = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("ADX_MFE_PAIR", pair)
+        for k in range(len(seqs)):
+            eng = native.Engine(seqs[k], [csts[k]], terms, aptamer=apt, fold_mode="mfe",
+                                thermostat=native.make_thermostat("fixed", t=1.0))
+            _, _, dg = eng.score_batch([seqs[k]])
+            got[(pair, k)] = [float(x) for x in dg[0]]
+            names = [eng.variant(v) for v in range(eng.info.n_variants)]
+    for k in range(len(seqs)):
+        assert got[("1", k)] == got[("0", k)], (N, k, got[("1", k)], got[("0", k)])
+        for v, (_, cond, mac) in enumerate(names):
+            ref = oracle.mfe_energy(seqs[k], csts[k] if mac >= 0 else None, motif if cond == 1 else None)
+            assert _same(got[("1", k)][v], ref), (N, k, v, got[("1", k)][v], ref)
+
+
+def test_pair_kernel_trajectory_matches_single(native, monkeypatch):
+    """A 4096-walker MC run at N = 100 (incremental refolds, the bench's
+    workload) with the pair kernel and with the one-diagonal kernel: identical
+    trajectories, scores and counters."""
+    tmpl, active = workloads.synthetic(100)
+    terms = workloads.default_objective()
+    seqs = workloads.walker_sequences(tmpl, [active], 4096)
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("ADX_MFE_PAIR", pair)
+        eng = _engine(native, tmpl, [active], terms,
+                      thermostat=native.make_thermostat("annealing", t_hi=5.0, t_lo=0.0, cycle_len=300))
+        eng.walkers_init(list(range(4096)), seqs)
+        eng.run_steps(40)
+        out[pair] = eng.download()
+        assert ("mfe_pair_kernel" in eng.last_kernel_names()[0]) == (pair == "1")
+    s1, sc1, c1 = out["1"]
+    s0, sc0, c0 = out["0"]
+    assert s1 == s0
+    assert (sc1 == sc0).all()
+    assert (c1 == c0).all()

@@ -30,6 +30,12 @@ def out_dir():
 
 
 MAXLOOP = 30
+# PAIR: the blocks of the two-diagonals-per-barrier kernel (mfe_pair.hip) --
+# loop sizes u >= 2 only (the stack and bulge-1 shapes run in its finalize), and
+# a lane-set holds cells of two diagonals d, d+1: a lane's inner cells sit at
+# off(d - 2 - u) + ci + hb * u, with ci = i + hb * (N - d + 2) and hb = 1 on the
+# lanes of diagonal d + 1 (per-lane, set once per lane-set)
+PAIR = False
 NBLK = int(os.environ.get("ADX_GEN_NBLK", "7"))   # block waves 0..NBLK-1 (wave 7 folds the multiloop qm / mla)
 SCHED_CHUNK = 1000 # shapes per scheduling window (whole loop sizes)
 KSAT = 5           # nin[k] == nin[KSAT] for k >= KSAT (checked on the host)
@@ -86,6 +92,13 @@ def scost(u, S):
 # wave 7, which has slack: 1.248M -> 1.266M MC steps/s; finalize on wave 1
 # instead of 6: +0.7-0.9 %; profiles/r04y_ab_roles.txt, r04z_ab_roles.txt)
 ROLES4 = "1:8,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
+# pair kernel: the finalize of two cells per lane on wave 1, q5 of two columns on
+# wave 3, the two-diagonal list on wave 4 (mfe_pair.hip)
+PAIR_ROLES4 = "1:14,3:6,4:12"
+
+
+def umin():
+    return 2 if PAIR else 0
 
 
 def role_loads(S):
@@ -93,7 +106,8 @@ def role_loads(S):
     Only the 4-lanes-per-cell partition uses them: it serves ~96 % of an MC
     refold's diagonals, the other two keep equal block costs."""
     init = [0] * NBLK
-    spec = os.environ.get("ADX_GEN_ROLES4", ROLES4) if S == 4 else ""
+    env = "ADX_GEN_PAIR_ROLES4" if PAIR else "ADX_GEN_ROLES4"
+    spec = os.environ.get(env, PAIR_ROLES4 if PAIR else ROLES4) if S == 4 else ""
     for item in filter(None, spec.split(",")):
         w, c = item.split(":")
         init[int(w)] = int(c)
@@ -102,7 +116,7 @@ def role_loads(S):
 
 def partition(S=1):
     # greedy LPT over loop sizes, largest first; ties keep small u spread out
-    sizes = sorted(range(MAXLOOP + 1), key=lambda u: (-scost(u, S), -ucost(u)))
+    sizes = sorted(range(umin(), MAXLOOP + 1), key=lambda u: (-scost(u, S), -ucost(u)))
     blocks = [[] for _ in range(NBLK)]
     load = role_loads(S)
     for u in sizes:
@@ -285,7 +299,7 @@ def sliced_parts(u, S, t):
     spec = [u1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen" and u1 not in ed]
     gen = [u1 for u1 in range(u + 1) if kind(u1, u - u1) == "gen"]
     pre, decl, lines, outs, ins, post = [], [], [], [], [], []
-    pre.append("const int o%s = off(dd - %d, U.N) + ci;" % (t, u + 2))
+    pre.append("const int o%s = off(dd - %d, U.N) + ci%s;" % (t, u + 2, (" + hb * %d" % u) if PAIR else ""))
     pre.append("const uint32_t qa%s = U.aq + uint32_t(o%s) * 4u, ka%s = U.ac + uint32_t(o%s);" % (t, t, t, t))
     ins += ['[qa%s] "v"(qa%s)' % (t, t), '[ka%s] "v"(ka%s)' % (t, t)]
     V = lambda u1: "v%d%s" % (u1, t)
@@ -456,9 +470,17 @@ def emit_block_cells_sliced(blk, S, out):
 
 
 def main():
+    global PAIR
+    for PAIR in (False, True):
+        emit_file()
+
+
+def emit_file():
     blocks, load = partition()
     out = []
     out.append("// GENERATED by tools/gen_mfe_blocks.py -- do not edit.")
+    if PAIR:
+        out.append("// Pair variant (mfe_pair.hip): loop sizes u >= 2, per-lane diagonal offset hb.")
     out.append("// Interior-loop shapes of mfe_cells.hip in %d blocks of LDS cost %s." % (NBLK, load))
     out.append("// Block b: loop sizes %s" % "; ".join("%d:%s" % (b, blk) for b, blk in enumerate(blocks)))
     out.append("")
@@ -468,6 +490,9 @@ def main():
         # above the block switch it would stay live across all blocks)
         out.append("    int ci = C.i, dd = U.d, um = U.umax;")
         out.append('    asm volatile("" : "+v"(ci));')
+        if PAIR:
+            out.append('    int hb = C.hb;')
+            out.append('    asm volatile("" : "+v"(hb));')
         out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
         out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
         out.append('    asm volatile("" : "+s"(kg));')
@@ -475,7 +500,7 @@ def main():
         for u in blk:
             out.append("    if (um < %d) goto fin;" % u)
             out.append("    {   // u = %d (batched reads)" % u)
-            out.append("        const int o = off(dd - %d, U.N) + ci;" % (u + 2))
+            out.append("        const int o = off(dd - %d, U.N) + ci%s;" % (u + 2, (" + hb * %d" % u) if PAIR else ""))
             out.append("        const uint32_t qa = U.aq + uint32_t(o) * 4u, ka = U.ac + uint32_t(o);")
             nspec = sum(1 for u1 in range(u + 1) if kind(u1, u - u1) != "gen")
             out.append("        uint32_t gk[6], fb = 0, f1n = 0, cs[%d];" % max(1, nspec))
@@ -501,6 +526,9 @@ def main():
             out.append("__device__ __forceinline__ void mfe_blk%d_s%d(const BUni &U, const BCell &C, Acc &a) {" % (b, S))
             out.append("    int ci = C.i, dd = U.d, um = U.umax, ea = C.ea, eb = C.eb;")
             out.append('    asm volatile("" : "+v"(ci), "+v"(ea), "+v"(eb));')
+            if PAIR:
+                out.append('    int hb = C.hb;')
+                out.append('    asm volatile("" : "+v"(hb));')
             out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
             out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
             out.append('    asm volatile("" : "+s"(kg));')
@@ -533,7 +561,7 @@ def main():
         "{%s}" % ", ".join(str(-1 if a is None else a) for a in row) for _, _, row in sl) or "{-1, -1, -1, -1}"))
     out.append("constexpr int MFE_NBLK = %d;" % NBLK)
     out.append("constexpr int MFE_KSAT = %d;   // generic loops: nin[k] == nin[MFE_KSAT] for k >= MFE_KSAT" % KSAT)
-    path = os.path.join(out_dir(), "mfe_blocks.inc")
+    path = os.path.join(out_dir(), "mfe_pair_blocks.inc" if PAIR else "mfe_blocks.inc")
     with open(path, "w") as f:
         f.write("\n".join(out) + "\n")
     print("blocks:", blocks, "load:", load, file=sys.stderr)
