@@ -758,7 +758,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             if (w0 || w1) {
                 __builtin_amdgcn_s_setprio(PRIO_ROLE);
                 const int s0 = L.S[j0], s1 = L.S[j1];
-                const int sp0 = L.S[j0 + 1], sp1 = (j1 < N) ? L.S[j1 + 1] : 5;   // j0 < N whenever j1 <= N
+                const int sp0 = (j0 < N) ? L.S[j0 + 1] : 5, sp1 = (j1 < N) ? L.S[j1 + 1] : 5;   // no dangle past N
                 u32 acc0 = INF16, acc1 = INF16;
                 for (int k0 = 1; k0 <= j1 - 4; k0 += WAVE) {
                     const int kk = k0 + lane;
