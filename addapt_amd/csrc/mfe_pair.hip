@@ -71,9 +71,9 @@ struct CP {
     u32 *dt;               // DT_* block (packed)
     uint8_t *cc;           // inner-pair code per cell (diagonal-major), pad before it
     uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
-    uint8_t *cl;           // [2][2 np]: rows of the pairable cells of a step's two diagonals, by step parity
-    int *cnt;              // [2][2]: cells of the step's first diagonal, of both
-    u32 *rec;              // [2][3][64]: the B cells' setup (rank < 64 over both diagonals) by step parity
+    uint8_t *cl;           // [3][2 np]: rows of the pairable cells of a step's two diagonals, by step % 3
+    int *cnt;              // [3][2]: cells of the step's first diagonal, of both
+    u32 *rec;              // [3][3][64]: the B cells' setup (rank < 64 over both diagonals) by step % 3
     u32 *e4;               // [MFE_E4_SLOTS][4]: per-slice generic energies of the 4-lane blocks
     int np;
 };
@@ -97,9 +97,9 @@ struct PLay {
     static constexpr size_t CC = DT + al16(size_t(DT_HP) * 4) + al16(NM - 3);   // span-3 codes before it
     static constexpr size_t BY = CC + al16(C);
     static constexpr size_t CLS = BY + al16(8 * NP);
-    static constexpr size_t CNT = CLS + al16(4 * NP);
-    static constexpr size_t REC = CNT + 16;
-    static constexpr size_t E4 = REC + 2 * 3 * 64 * 4;
+    static constexpr size_t CNT = CLS + al16(6 * NP);
+    static constexpr size_t REC = CNT + 32;
+    static constexpr size_t E4 = REC + 3 * 3 * 64 * 4;
     static constexpr size_t BYTES = E4 + size_t(MFE_E4_MAX) * 16;
     __device__ static CP carve(char *b) {
         CP l;
@@ -334,57 +334,84 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     U.nin = reinterpret_cast<const u32 *>(XS->nin);
     U.N = N;
     const uint32_t aqm = lds_addr(L.qm), aqm1 = lds_addr(L.qm1), ae4 = lds_addr(L.e4);
-    constexpr int L_WAVE = 4;           // the list of the next step's two diagonals and their B records
+    constexpr int L_WAVE = 4;           // the lists two steps ahead (diagonals d+4, d+5) and their B records
     constexpr int Q_WAVE = 3;           // q5 of two columns
-    constexpr int fw[2] = {1, 5};       // finalize lane-sets 0, 1 (rows 1..64, 64..127)
+    constexpr int fw[2] = {MA_WAVE, 5}; // finalize lane-sets 0, 1 (rows 1..64, 64..127): the split-part
+                                        // wave has no blocks, lane-set 1 (spans < 38) rides on block wave 5
     int fls = -1;
     for (int k = 0; k < 2; k++)
         if (fw[k] == wid) fls = k;
+    const int NP2 = 2 * NP;
+    // the pairable cells of diagonals db, db+1 (ranks < P0 on db) and the B records of
+    // ranks < 64 into list slot sl (a step's B reads them two steps later: its first
+    // lane-set's records are loaded a step ahead, across the barrier)
+    auto build_list = [&](int db, int sl) {
+        int base = 0, P0 = 0;
+        for (int k = 0; k < 2; k++) {
+            const int dn = db + k;
+            if (k == 1) P0 = base;
+            if (dn < 8 || dn > N - 1) continue;   // interior loops u >= 2 need spans >= 8
+            const int lo = clo(dn), hi = chi(dn);
+            const int Ln = lanesets(hi - lo + 1);
+            for (int ls = 0; ls < Ln; ls++) {
+                const int i = lo + ls * WAVE + lane;
+                const bool pr = i <= hi && L.qbm[off(dn, N) + i - 1] != MARK16;
+                const uint64_t m = __ballot(pr);
+                const int rk = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                if (pr) L.cl[sl * NP2 + rk] = uint8_t(i);
+                if (pr && rk < WAVE) {
+                    const int j = i + dn;
+                    const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
+                    const u32 mmo = L.dt[DT_MMI + oc];
+                    u32 *rr = L.rec + sl * 3 * WAVE + rk;
+                    rr[0] = uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) |
+                            (uint32_t(L.dn[j - 1]) << 24);
+                    rr[WAVE] = mmo;
+                    rr[2 * WAVE] = padd(L.ct[CT_ONEN + oc], mmo);
+                }
+                base += __popcll(m);
+            }
+        }
+        if (lane == 0) {
+            L.cnt[2 * sl] = P0;
+            L.cnt[2 * sl + 1] = base;
+        }
+    };
+    if (wid == L_WAVE) {   // steps 0 (no B work: d + 1 < 8) and 1
+        if (lane == 0) L.cnt[0] = L.cnt[1] = 0;
+        build_list(8, 1);
+    }
+    __syncthreads();
+    // the first lane-set's B record of the next step, loaded a step ahead
+    auto slices = [](int P) { return P <= 16 ? 2 : (P <= 32 ? 1 : 0); };   // log2 slices per cell
+    int pP0 = 0, pP = 0;
+    u32 pwd = 0, pmmo = 0, pmo = 0;
+    auto prefetch = [&](int sl) {
+        pP0 = uni(L.cnt[2 * sl]);
+        pP = uni(L.cnt[2 * sl + 1]);
+        const int idx = lane & ((1 << (6 - slices(pP))) - 1);
+        if (idx < pP) {
+            const u32 *rr = L.rec + sl * 3 * WAVE + idx;
+            pwd = rr[0];
+            pmmo = rr[WAVE];
+            pmo = rr[2 * WAVE];
+        }
+    };
 
 #ifdef ADX_STAMP
     unsigned long long st_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
     st_acc[8] = st_last - st_setup0;
 #endif
-    const int NP2 = 2 * NP;
+    int sl = 0;   // list slot of this step: step index % 3
     for (int d = 6; d - 3 <= N; d += 2) {
-        const int par = (d >> 1) & 1;
+        const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;
         PSTAMP(0);
-        // ---------------- L: the pairable cells of diagonals d+2, d+3 (B's lanes next
-        // step; their qbm marks are the setup's) and the records of ranks < 64
+        // ---------------- L: the pairable cells of diagonals d+4, d+5 (B's lanes two
+        // steps on; their qbm marks are the setup's) and the records of ranks < 64
         if (wid == L_WAVE) {
             __builtin_amdgcn_s_setprio(PRIO_ROLE);
-            const int pn = 1 - par;
-            int base = 0, P0 = 0;
-            for (int k = 0; k < 2; k++) {
-                const int dn = d + 2 + k;
-                if (k == 1) P0 = base;
-                if (dn > N - 1) continue;
-                const int lo = clo(dn), hi = chi(dn);
-                const int Ln = lanesets(hi - lo + 1);
-                for (int ls = 0; ls < Ln; ls++) {
-                    const int i = lo + ls * WAVE + lane;
-                    const bool pr = i <= hi && L.qbm[off(dn, N) + i - 1] != MARK16;
-                    const uint64_t m = __ballot(pr);
-                    const int rk = base + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                    if (pr) L.cl[pn * NP2 + rk] = uint8_t(i);
-                    if (pr && rk < WAVE) {
-                        const int j = i + dn;
-                        const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
-                        const u32 mmo = L.dt[DT_MMI + oc];
-                        u32 *rr = L.rec + pn * 3 * WAVE + rk;
-                        rr[0] = uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) |
-                                (uint32_t(L.dn[j - 1]) << 24);
-                        rr[WAVE] = mmo;
-                        rr[2 * WAVE] = padd(L.ct[CT_ONEN + oc], mmo);
-                    }
-                    base += __popcll(m);
-                }
-            }
-            if (lane == 0) {
-                L.cnt[2 * pn] = P0;
-                L.cnt[2 * pn + 1] = base;
-            }
+            build_list(d + 4, sl2);
             __builtin_amdgcn_s_setprio(0);
         }
         PSTAMP(1);
@@ -563,8 +590,8 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         // the rest on d+1); a lane of d+1 reads its inner cells at
         // off(d - 2 - u) + i + (N - d + 2 + u), which the blocks add per lane (hb).
         if (d + 1 >= 8 && d <= N - 1) {
-            const int P0 = L.cnt[2 * par], P = L.cnt[2 * par + 1];
-            const int sh = P <= 16 ? 2 : (P <= 32 ? 1 : 0);   // log2 slices per cell
+            const int P0 = pP0, P = pP;
+            const int sh = slices(P);
             const int cwl = 6 - sh;
             const int Lb = (P + (1 << cwl) - 1) >> cwl;
             const int blk = wid;
@@ -578,8 +605,16 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     const int dd = d + hb;
                     int i, oc, cA, cB;
                     u32 mmo, mo;
-                    if (idx < WAVE) {
-                        const u32 *rr = L.rec + par * 3 * WAVE + idx;
+                    if (ls == 0) {   // loaded a step ahead
+                        const u32 wd = pwd;
+                        mmo = pmmo;
+                        mo = pmo;
+                        i = wd & 255;
+                        oc = (wd >> 8) & 255;
+                        cA = (wd >> 16) & 255;
+                        cB = wd >> 24;
+                    } else if (idx < WAVE) {
+                        const u32 *rr = L.rec + sl * 3 * WAVE + idx;
                         const u32 wd = rr[0];
                         mmo = rr[WAVE];
                         mo = rr[2 * WAVE];
@@ -588,7 +623,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                         cA = (wd >> 16) & 255;
                         cB = wd >> 24;
                     } else {
-                        i = L.cl[par * NP2 + idx];
+                        i = L.cl[sl * NP2 + idx];
                         oc = ptype(L.S[i], L.S[i + dd]) * 25 + L.S[i + 1] * 5 + L.S[i + dd - 1];
                         cA = L.up[i + 1];
                         cB = L.dn[i + dd - 1];
@@ -655,6 +690,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                 }
             }
         }
+        if (wid < MFE_NBLK) prefetch(sl1);   // the next step's list was built a step ago
         PSTAMP(3);
         // ---------------- M: split parts of qm for spans d and d+1 (lanes = cells x
         // slices of the split points, mfe_cells.hip): min over t >= 5 of
@@ -790,6 +826,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         PSTAMP(5);
         lds_barrier();
         PSTAMP(6);
+        sl = sl1;
     }
 #ifdef ADX_STAMP
     if (lane == 0 && wid < 16)

@@ -15,7 +15,7 @@ T=$(mktemp -d)
 H="hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC"
 $H -c $SRC/adx_api.cpp -o $OUT/api.o &
 $H -c $SRC/energy.cpp -o $OUT/energy.o &
-for f in kernels.hip mfe_cells.hip outside_cells.hip pf_cells.hip pf_ring.hip outside_ring.hip; do
+for f in kernels.hip mfe_cells.hip mfe_pair.hip outside_cells.hip pf_cells.hip pf_ring.hip outside_ring.hip; do
   $H -c $SRC/$f -o $OUT/tree_${f%.hip}.o &
 done
 wait
@@ -32,7 +32,7 @@ for spec in "$@"; do
   (
   for f in $files; do $H $flags -c $T/$name/$f -o $OUT/${name}_${f%.hip}.o; done
   objs=""
-  for f in kernels mfe_cells outside_cells pf_cells pf_ring outside_ring; do
+  for f in kernels mfe_cells mfe_pair outside_cells pf_cells pf_ring outside_ring; do
     if [[ " $files " == *" $f.hip "* ]]; then objs="$objs $OUT/${name}_$f.o"; else objs="$objs $OUT/tree_$f.o"; fi
   done
   hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_$name.so $objs $OUT/api.o $OUT/energy.o

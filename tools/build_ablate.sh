@@ -14,6 +14,7 @@ for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}; flags=${flags//__/ }
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c kernels.hip -o $OUT/k_$name.o &
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c mfe_cells.hip -o $OUT/c_$name.o &
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c mfe_pair.hip -o $OUT/m_$name.o &
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c outside_cells.hip -o $OUT/o_$name.o &
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c pf_cells.hip -o $OUT/p_$name.o &
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $flags -c pf_ring.hip -o $OUT/r_$name.o &
@@ -22,5 +23,5 @@ done
 wait
 for v in $VARIANTS; do
   name=${v%%:*}
-  hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_$name.so $OUT/k_$name.o $OUT/c_$name.o $OUT/o_$name.o $OUT/p_$name.o $OUT/r_$name.o $OUT/q_$name.o $OUT/api.o $OUT/energy.o
+  hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/lib_$name.so $OUT/k_$name.o $OUT/c_$name.o $OUT/m_$name.o $OUT/o_$name.o $OUT/p_$name.o $OUT/r_$name.o $OUT/q_$name.o $OUT/api.o $OUT/energy.o
 done

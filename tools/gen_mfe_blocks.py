@@ -92,9 +92,10 @@ def scost(u, S):
 # wave 7, which has slack: 1.248M -> 1.266M MC steps/s; finalize on wave 1
 # instead of 6: +0.7-0.9 %; profiles/r04y_ab_roles.txt, r04z_ab_roles.txt)
 ROLES4 = "1:8,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
-# pair kernel: the finalize of two cells per lane on wave 1, q5 of two columns on
-# wave 3, the two-diagonal list on wave 4 (mfe_pair.hip)
-PAIR_ROLES4 = "1:14,3:6,4:12"
+# pair kernel: q5 of two columns on wave 3, the two-diagonal list on wave 4, the
+# finalize's second lane-set (spans < 38) on wave 5 (mfe_pair.hip; its first
+# lane-set runs on the split-part wave 7)
+PAIR_ROLES4 = "3:6,4:12,5:3"
 
 
 def umin():
