@@ -47,10 +47,12 @@ __device__ unsigned long long g_stamps_p[16][16];
 
 namespace {
 
-// waves per walker: 0..6 interior-loop blocks, 7 the split parts of qm; the
-// finalize, list and q5 roles ride on block waves (two workgroups per CU)
+// waves per walker: 0..6 interior-loop blocks, 7 the finalize; the split parts
+// of qm (one span per wave), the lists and q5 ride on block waves, whose loop
+// sizes the generator partitions around them (tools/gen_mfe_blocks.py
+// PAIR_ROLES4; two workgroups per CU)
 constexpr int NWV = 8;
-constexpr int MA_WAVE = 7;
+constexpr int F_WAVE = 7;
 constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
 
 #include "mfe_pair_blocks.inc"
@@ -72,8 +74,10 @@ struct CP {
     uint8_t *cc;           // inner-pair code per cell (diagonal-major), pad before it
     uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
     uint8_t *cl;           // [3][2 np]: rows of the pairable cells of a step's two diagonals, by step % 3
-    int *cnt;              // [3][2]: cells of the step's first diagonal, of both
-    u32 *rec;              // [3][3][64]: the B cells' setup (rank < 64 over both diagonals) by step % 3
+    int *cnt;              // [3]: cells of the step's first diagonal | of both << 16
+    u32 *rec;              // [3][2][64]: the B cells' setup (rank < 64 over both diagonals) by step % 3:
+                           //   i | oc << 8 | A << 16 | B << 24 and mismatchI(oc) | mismatch1n(oc) +
+                           //   mismatchI(oc) << 16 (MFE table entries are equal in both halves)
     u32 *e4;               // [MFE_E4_SLOTS][4]: per-slice generic energies of the 4-lane blocks
     int np;
 };
@@ -98,8 +102,8 @@ struct PLay {
     static constexpr size_t BY = CC + al16(C);
     static constexpr size_t CLS = BY + al16(8 * NP);
     static constexpr size_t CNT = CLS + al16(6 * NP);
-    static constexpr size_t REC = CNT + 32;
-    static constexpr size_t E4 = REC + 3 * 3 * 64 * 4;
+    static constexpr size_t REC = CNT + 16;
+    static constexpr size_t E4 = REC + 3 * 2 * 64 * 4;
     static constexpr size_t BYTES = E4 + size_t(MFE_E4_MAX) * 16;
     __device__ static CP carve(char *b) {
         CP l;
@@ -336,8 +340,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const uint32_t aqm = lds_addr(L.qm), aqm1 = lds_addr(L.qm1), ae4 = lds_addr(L.e4);
     constexpr int L_WAVE = 4;           // the lists two steps ahead (diagonals d+4, d+5) and their B records
     constexpr int Q_WAVE = 3;           // q5 of two columns
-    constexpr int fw[2] = {MA_WAVE, 5}; // finalize lane-sets 0, 1 (rows 1..64, 64..127): the split-part
-                                        // wave has no blocks, lane-set 1 (spans < 38) rides on block wave 5
+    constexpr int fw[2] = {F_WAVE, 6};  // finalize lane-sets 0, 1 (rows 1..64, 64..127): lane-set 1
+                                        // (spans < 38) rides on block wave 6
+    constexpr int mw[2] = {0, 2};       // the split parts of spans d, d+1
     int fls = -1;
     for (int k = 0; k < 2; k++)
         if (fw[k] == wid) fls = k;
@@ -363,40 +368,38 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     const int j = i + dn;
                     const int oc = ptype(L.S[i], L.S[j]) * 25 + L.S[i + 1] * 5 + L.S[j - 1];
                     const u32 mmo = L.dt[DT_MMI + oc];
-                    u32 *rr = L.rec + sl * 3 * WAVE + rk;
+                    u32 *rr = L.rec + sl * 2 * WAVE + rk;
                     rr[0] = uint32_t(i) | (uint32_t(oc) << 8) | (uint32_t(L.up[i + 1]) << 16) |
                             (uint32_t(L.dn[j - 1]) << 24);
-                    rr[WAVE] = mmo;
-                    rr[2 * WAVE] = padd(L.ct[CT_ONEN + oc], mmo);
+                    rr[WAVE] = (mmo & 0xFFFFu) | (padd(L.ct[CT_ONEN + oc], mmo) << 16);
                 }
                 base += __popcll(m);
             }
         }
-        if (lane == 0) {
-            L.cnt[2 * sl] = P0;
-            L.cnt[2 * sl + 1] = base;
-        }
+        if (lane == 0) L.cnt[sl] = P0 | (base << 16);
     };
     if (wid == L_WAVE) {   // steps 0 (no B work: d + 1 < 8) and 1
-        if (lane == 0) L.cnt[0] = L.cnt[1] = 0;
+        if (lane == 0) L.cnt[0] = 0;
         build_list(8, 1);
     }
     __syncthreads();
     // the first lane-set's B record of the next step, loaded a step ahead
     auto slices = [](int P) { return P <= 16 ? 2 : (P <= 32 ? 1 : 0); };   // log2 slices per cell
-    int pP0 = 0, pP = 0;
-    u32 pwd = 0, pmmo = 0, pmo = 0;
-    auto prefetch = [&](int sl) {
-        pP0 = uni(L.cnt[2 * sl]);
-        pP = uni(L.cnt[2 * sl + 1]);
-        const int idx = lane & ((1 << (6 - slices(pP))) - 1);
-        if (idx < pP) {
-            const u32 *rr = L.rec + sl * 3 * WAVE + idx;
-            pwd = rr[0];
-            pmmo = rr[WAVE];
-            pmo = rr[2 * WAVE];
-        }
+    int cPP = 0;                // this step's list counts (CP::cnt), loaded a step ahead,
+    u32 cwd = 0, cmm = 0;       // and its first lane-set's B record
+    // loaded at the top of the step before (issued with nothing to wait on: they
+    // complete under the step's first read batch); the records of the 4-lanes-
+    // per-cell mapping (lane & 15), the one of ~96 % of a refold's steps -- B
+    // reads its records itself when the step maps its lanes otherwise
+    auto load_list = [&](int sl, int &PP, u32 &wd, u32 &mm) {
+        PP = L.cnt[sl];
+        const u32 *rr = L.rec + sl * 2 * WAVE + (lane & 15);
+        wd = rr[0];
+        mm = rr[WAVE];
     };
+    // the record's two energies, each 16 bits wide, to packed apo | holo words
+    auto lo2 = [](u32 x) { return __builtin_amdgcn_perm(x, x, 0x05040504u); };
+    auto hi2 = [](u32 x) { return __builtin_amdgcn_perm(x, x, 0x07060706u); };
 
 #ifdef ADX_STAMP
     unsigned long long st_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -407,6 +410,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     for (int d = 6; d - 3 <= N; d += 2) {
         const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;
         PSTAMP(0);
+        int nPP = 0;
+        u32 nwd = 0, nmm = 0;
+        if (wid < MFE_NBLK) load_list(sl1, nPP, nwd, nmm);   // the next step's, built a step ago
         // ---------------- L: the pairable cells of diagonals d+4, d+5 (B's lanes two
         // steps on; their qbm marks are the setup's) and the records of ranks < 64
         if (wid == L_WAVE) {
@@ -590,7 +596,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         // the rest on d+1); a lane of d+1 reads its inner cells at
         // off(d - 2 - u) + i + (N - d + 2 + u), which the blocks add per lane (hb).
         if (d + 1 >= 8 && d <= N - 1) {
-            const int P0 = pP0, P = pP;
+            const int P0 = uni(cPP & 0xFFFF), P = uni(cPP >> 16);
             const int sh = slices(P);
             const int cwl = 6 - sh;
             const int Lb = (P + (1 << cwl) - 1) >> cwl;
@@ -605,19 +611,19 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     const int dd = d + hb;
                     int i, oc, cA, cB;
                     u32 mmo, mo;
-                    if (ls == 0) {   // loaded a step ahead
-                        const u32 wd = pwd;
-                        mmo = pmmo;
-                        mo = pmo;
+                    if (ls == 0 && sh == 2) {   // loaded a step ahead
+                        const u32 wd = cwd;
+                        mmo = lo2(cmm);
+                        mo = hi2(cmm);
                         i = wd & 255;
                         oc = (wd >> 8) & 255;
                         cA = (wd >> 16) & 255;
                         cB = wd >> 24;
                     } else if (idx < WAVE) {
-                        const u32 *rr = L.rec + sl * 3 * WAVE + idx;
+                        const u32 *rr = L.rec + sl * 2 * WAVE + idx;
                         const u32 wd = rr[0];
-                        mmo = rr[WAVE];
-                        mo = rr[2 * WAVE];
+                        mmo = lo2(rr[WAVE]);
+                        mo = hi2(rr[WAVE]);
                         i = wd & 255;
                         oc = (wd >> 8) & 255;
                         cA = (wd >> 16) & 255;
@@ -690,15 +696,16 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                 }
             }
         }
-        if (wid < MFE_NBLK) prefetch(sl1);   // the next step's list was built a step ago
+        cPP = nPP, cwd = nwd, cmm = nmm;
         PSTAMP(3);
         // ---------------- M: split parts of qm for spans d and d+1 (lanes = cells x
         // slices of the split points, mfe_cells.hip): min over t >= 5 of
         // qm(i, i+t-1) + qm1(i+t, j), written to the span's slot for F
-        if (wid == MA_WAVE) {
+        if (wid == mw[0] || wid == mw[1]) {
             __builtin_amdgcn_s_setprio(PRIO_ROLE);
-            for (int s = d; s <= d + 1; s++) {
-                if (s < 9 || s > N - 3) continue;   // no split point below span 9
+            {
+                const int s = wid == mw[0] ? d : d + 1;
+                if (s >= 9 && s <= N - 3) {   // no split point below span 9
                 const int lo = qlo(s), hi = qhi(s);
                 const int Lm = lanesets(hi - lo + 1);
                 const int Tt = s - 4;
@@ -781,6 +788,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     u32 split = pmin(sp0, sp1);
                     for (int k = cst; k < WAVE; k <<= 1) split = pmin(split, u32(__shfl_xor(int(split), k, WAVE)));
                     if (valid && rr == 0) slot[i] = pfin(split);
+                }
                 }
             }
             __builtin_amdgcn_s_setprio(0);

@@ -67,6 +67,9 @@ def parse():
                     help="replica exchange: each rank writes DIR/rank<r>.npz with per-round configuration "
                          "digests before/after the swap and sampled final walkers (tests; off the timed path "
                          "only in the sense that it adds host copies per round)")
+    ap.add_argument("--dump-walkers", default=None, metavar="DIR",
+                    help="each rank writes DIR/rank<r>.npz with its global walker ids and final sequences, "
+                         "scores and counters (after the timed region; tests of G-independence)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) of this workload, fills roofline.traffic "
                          "(default profiles/traffic_latest_<fold>.json)")
@@ -260,7 +263,7 @@ def executed_inside_work(eng, cur_seqs, tmpl, active, fold, sample=32):
 
 
 def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, dev, local_rank,
-            traffic_json=None, cpu=False, cpu_seconds=15.0):
+            traffic_json=None, cpu=False, cpu_seconds=15.0, dump=None):
     """Run one workload (W walkers of this rank) and return its record: value
     (all ranks), ms_per_step, roofline of the dominant kernel, outcomes."""
     from addapt_amd import native, roofline, shard, workloads
@@ -319,6 +322,14 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     inside_name, outside_name = eng.last_kernel_names()  # what the engine launched
     fin_seqs, fin_scores, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device=dev)
+    if dump:
+        import numpy as np
+
+        os.makedirs(dump, exist_ok=True)
+        np.savez(os.path.join(dump, "rank%d.npz" % rank), gids=np.array(gids_rank), seqs=np.array(fin_seqs),
+                 scores=fin_scores, counters=c1, template=np.array([tmpl]), active=np.array([active]),
+                 fold=np.array([fold]), bppm=np.array([bppm]), length=np.array([length]),
+                 kernels=np.array([eng.last_kernel_names()[0], eng.last_kernel_names()[1]]))
     # executed (incremental) vs algorithmic inside work, from one traced step
     # after the timed region (rank 0 reports it)
     ex_inside, full_inside, ex_n = executed_inside_work(eng, fin_seqs, tmpl, active, fold) \
@@ -522,7 +533,8 @@ def main():
     W = a.walkers
     gids = shard.walker_ids(rank, world, W)
     rec = measure(a, a.fold, a.bppm, a.length, a.steps, a.warmup, rank, world, gids, dist, dev, device,
-                  traffic_json=a.traffic_json, cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds)
+                  traffic_json=a.traffic_json, cpu=not a.no_cpu_baseline, cpu_seconds=a.cpu_seconds,
+                  dump=a.dump_walkers)
     out = {
         "metric": METRIC,
         "value": rec["value"],

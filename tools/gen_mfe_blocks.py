@@ -92,10 +92,11 @@ def scost(u, S):
 # wave 7, which has slack: 1.248M -> 1.266M MC steps/s; finalize on wave 1
 # instead of 6: +0.7-0.9 %; profiles/r04y_ab_roles.txt, r04z_ab_roles.txt)
 ROLES4 = "1:8,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
-# pair kernel: q5 of two columns on wave 3, the two-diagonal list on wave 4, the
-# finalize's second lane-set (spans < 38) on wave 5 (mfe_pair.hip; its first
-# lane-set runs on the split-part wave 7)
-PAIR_ROLES4 = "3:6,4:12,5:3"
+# pair kernel (mfe_pair.hip; cycles from tools/mfe_pair_stamps.py at ~4k per
+# unit): the split parts of span d on wave 0 and of d+1 on wave 2, q5 of two
+# columns on wave 3, the lists on wave 4, the finalize's second lane-set
+# (spans < 38) on wave 6; its first lane-set has wave 7 to itself
+PAIR_ROLES4 = "0:22,2:22,3:16,4:22,6:5"
 
 
 def umin():
@@ -362,8 +363,13 @@ def sliced_parts(u, S, t):
         post.append("    %s = (%d >= ml && %d <= mh) ? %s : INF16;" % (V(u1), u1, u1, V(u1)))
     for nm, _, _ in eds:
         post.append("    v%s%s = (n%s%s >= ml && n%s%s <= mh) ? v%s%s : INF16;" % ((nm, t) * 4))
+    if PAIR and nk:   # the slice offset folded into the bounds once (no per-position lane constants)
+        post.append("    const int gl = ml - rr, gh = mh - rr;")
     for k in range(nk):
-        post.append("    w%d%s = (%d + rr >= ml && %d + rr <= mh) ? w%d%s : INF16;" % (k, t, gen[0] + S * k, gen[0] + S * k, k, t))
+        if PAIR:
+            post.append("    w%d%s = (%d >= gl && %d <= gh) ? w%d%s : INF16;" % (k, t, gen[0] + S * k, gen[0] + S * k, k, t))
+        else:
+            post.append("    w%d%s = (%d + rr >= ml && %d + rr <= mh) ? w%d%s : INF16;" % (k, t, gen[0] + S * k, gen[0] + S * k, k, t))
     post.append("}")
     if gen:
         post.append("const uint32_t gk%s[6] = {kr0%s.x, kr0%s.y, kr0%s.z, kr0%s.w, kr1%s.x, kr1%s.y};" % ((t,) * 7))
