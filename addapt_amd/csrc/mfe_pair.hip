@@ -60,6 +60,14 @@ static_assert(MFE_NBLK == 7, "seven block waves");
 
 constexpr int PINF = 32767;   // an impossible half, sign-extended (the partial slots)
 
+// bit 8 * log2(lanes per cell) + b: block b reads loop size u in that mode
+constexpr unsigned size_bits(int u) {
+    unsigned m = 0;
+    for (int s = 0; s < 3; s++)
+        if (MFE_SIZE_BLOCK[s][u] >= 0) m |= 1u << (8 * s + MFE_SIZE_BLOCK[s][u]);
+    return m;
+}
+
 // ---------------------------------------------------------------- LDS carve
 struct CP {
     u32 *qbm, *qm, *qm1;   // cell tables (fold_common.hpp indexing); qbm has an
@@ -654,23 +662,25 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     C.A = cA;
                     C.B = cB;
                     const u32 tau = type > 2 ? tauE : 0u;
-                    C.m23f = padd(L.ct[CT_M23O + oc], fsm5);
+                    // the loop sizes' table energies only on the wave whose block reads them
+                    // (bits of a literal: a runtime-indexed table would be a scalar load)
+                    auto has = [&](unsigned bits) { return ((bits >> (sh * 8 + blk)) & 1u) != 0; };
+                    C.m23f = has(size_bits(5)) ? padd(L.ct[CT_M23O + oc], fsm5) : INF16;
                     C.t11 = C.t12 = C.t21 = C.t22 = INF16;
-                    const unsigned tbm = sh == 2 ? MFE_TABLE_BLOCKS_S4 : sh == 1 ? MFE_TABLE_BLOCKS_S2 : MFE_TABLE_BLOCKS;
-                    if ((tbm >> blk) & 1) {   // 1x1..2x2 energies from HBM (L2), used at the block end
+                    {   // 1x1..2x2 energies from HBM (L2), used at the block end
                         const int ty8 = type * 8;
-                        if (uml >= 2) {
+                        if (has(size_bits(2)) && uml >= 2) {
                             const int c2 = L.cc[off(dd - 4, N) + i + 1];
                             C.t11 = T11[((ty8 + ((c2 * 41) >> 10)) * 5 + si1) * 5 + sj1];
                         }
-                        if (uml >= 3) {
+                        if (has(size_bits(3)) && uml >= 3) {
                             const int o3 = off(dd - 5, N) + i;
                             const int a2 = L.cc[o3 + 1], b2 = L.cc[o3 + 2];
                             const int ta = (a2 * 41) >> 10, tb = (b2 * 41) >> 10;
                             C.t12 = T21[(((ty8 + ta) * 5 + si1) * 5 + (a2 / 5) % 5) * 5 + sj1];
                             C.t21 = T21[(((tb * 8 + type) * 5 + (b2 / 5) % 5) * 5 + si1) * 5 + b2 % 5];
                         }
-                        if (uml >= 4) {
+                        if (has(size_bits(4)) && uml >= 4) {
                             const int c2 = L.cc[off(dd - 6, N) + i + 2];
                             const int t2 = (c2 * 41) >> 10;
                             C.t22 = T22[((((ty8 + t2) * 5 + si1) * 5 + c2 % 5) * 5 + (c2 / 5) % 5) * 5 + sj1];

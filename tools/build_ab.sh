@@ -3,7 +3,7 @@
 # name=<git rev or "tree">:<kernel files, comma-separated>:<flags> replaces those
 # kernel sources by their version at that revision (the rest is the working
 # tree; host code and headers always from the tree) and adds the flags
-# ("__" for spaces).  Select one with ADX_LIB=addapt_amd/_lib/ablate/lib_<name>.so
+# ("__" for spaces); generated includes (*.inc) in the list are replaced too.  Select one with ADX_LIB=addapt_amd/_lib/ablate/lib_<name>.so
 # (tools/gpu_run.sh "libs" step).
 #   tools/build_ab.sh new=tree:mfe_cells.hip: old=HEAD:mfe_cells.hip: stamp=tree:mfe_cells.hip:-DADX_STAMP
 set -e
@@ -30,7 +30,7 @@ for spec in "$@"; do
     for f in $files; do git -C $ROOT show $rev:addapt_amd/csrc/$f > $T/$name/$f; done
   fi
   (
-  for f in $files; do $H $flags -c $T/$name/$f -o $OUT/${name}_${f%.hip}.o; done
+  for f in $files; do case $f in *.hip) $H $flags -c $T/$name/$f -o $OUT/${name}_${f%.hip}.o ;; esac; done
   objs=""
   for f in kernels mfe_cells mfe_pair outside_cells pf_cells pf_ring outside_ring; do
     if [[ " $files " == *" $f.hip "* ]]; then objs="$objs $OUT/${name}_$f.o"; else objs="$objs $OUT/tree_$f.o"; fi

@@ -559,6 +559,17 @@ def emit_file():
                 tb |= 1 << b
         out.append("constexpr unsigned MFE_TABLE_BLOCKS%s = 0x%xu;   // blocks with 1x1 / 1x2 / 2x1 / 2x2 shapes%s"
                    % ("" if S == 1 else "_S%d" % S, tb, "" if S == 1 else " (%d lanes per cell)" % S))
+    # the block (wave) of every loop size per lanes-per-cell mode (1, 2, 4): the
+    # kernels load a table energy / factor only on the wave whose block reads it
+    rows = []
+    for S in (1, 2, 4):
+        wb = [-1] * (MAXLOOP + 1)
+        for b, blk in enumerate(partition(S)[0]):
+            for u in blk:
+                wb[u] = b
+        rows.append("{%s}" % ", ".join(str(x) for x in wb))
+    out.append("constexpr signed char MFE_SIZE_BLOCK[3][%d] = {%s};   // [log2 lanes per cell][u] -> block"
+               % (MAXLOOP + 1, ", ".join(rows)))
     sl = e4_slots() if ETAB4 else []
     out.append("// per-lane generic energies of the 4-lanes-per-cell blocks: slot q holds loop size")
     out.append("// MFE_E4_U[q] and, for slice r, the Ninio index MFE_E4_A[q][r] (-1: no shape)")
