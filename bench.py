@@ -435,8 +435,17 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         # incremental refold (read back for the unchanged cells, <= the same again)
         "algorithmic_bytes_per_launch": scored_pl * (length + 8 + 2 * state_bytes),
         "state_bytes_per_scored_walker": state_bytes,
+        # the priced kernel's own compulsory bytes, comparable with `traffic` (its PMC
+        # bytes): the inside folds' as above; the outside pass reads the stored inside
+        # tables of the apo / holo unconstrained folds (3 cell tables + q5, FP32)
+        "priced_kernel_algorithmic_bytes_per_launch": (
+            scored_pl * 2 * (3 * cells + length + 2) * 4 if outside_dominant
+            else scored_pl * (length + 8 + 2 * state_bytes)),
+        "traffic_over_algorithmic": None,
         "hbm_peak_GBps": HBM_PEAK_GBPS,
     }
+    if traffic and roof["priced_kernel_algorithmic_bytes_per_launch"]:
+        roof["traffic_over_algorithmic"] = traffic / roof["priced_kernel_algorithmic_bytes_per_launch"]
     rec = {
         "value": value,
         "unit": "MC steps/s",

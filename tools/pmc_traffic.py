@@ -17,7 +17,7 @@ import sys
 
 # the kernels of one step's score window (kernels.hip, mfe_cells.hip, pf_cells.hip, outside_cells.hip):
 # the fold kernels, and with pair terms the outside pass and the score combine
-SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "pf_cells_kernel", "pf_ring_kernel", "outside_cells_kernel",
+SCORE_KERNELS = ("score_kernel", "mfe_cells_kernel", "mfe_pair_kernel", "pf_cells_kernel", "pf_ring_kernel", "outside_cells_kernel",
                  "outside_ring_kernel", "bppm_kernel", "combine_kernel")
 
 
