@@ -96,7 +96,7 @@ struct PxLay {
         Q1 = o;   o += a16((size_t(C) + PX_SLACK) * 8);           // qm1, column-major
         CC = o;   o += a16(size_t(C) + PX_SLACK);                 // inner-pair code per cell
         PART = o; o += a16(size_t(2) * 2 * PX_NB * WAVE * 8);     // [parity][lane-set][block][lane]
-        REC = o;  o += a16(size_t(2) * 2 * PX_RF * WAVE * 4 + 16); // [parity][set][field][lane]; counts
+        REC = o;  o += a16(size_t(3) * 2 * PX_RF * WAVE * 4 + 16); // [diagonal % 3][set][field][lane]; counts
         CL = o;   o += a16(size_t(C) + size_t(NP));               // rank lists of the changed pairable cells + counts
         MLA = o;  o += a16(size_t(2) * NP * 8);                   // split part of qm, by span parity
         UC = o;   o += a16(size_t(2) * NP * 8);                   // unpaired part U(i, j) of qm by column j, by span parity
@@ -349,33 +349,70 @@ __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int 
     px_load<U3>(s3, XS, r);
     px_load<U4>(s4, XS, r);
     const int ctb = r < 2 ? CT_BUL : CT_ONEN;   // the lane's special-shape inner factor table
+    // the first lane-set's records and the count of diagonal D, loaded a step
+    // ahead (the record wave writes them two steps ahead, slot D % 3): issued
+    // at the top of a step, they complete under its first reads
+    struct Pre {
+        int n, fl;
+        float mmo, mo, m23, t11, t12, t21, t22;
+    };
+    auto pre_load = [&](int D) {
+        Pre p;
+        const int sl = D % 3;
+        p.n = (D <= N - 1 && D >= 6) ? L.rcnt[sl] : 0;
+        const float *rr = L.rec + (sl * 2 * PX_RF) * WAVE + cq;
+        p.fl = __float_as_int(rr[0]);
+        p.mmo = rr[WAVE];
+        p.mo = rr[2 * WAVE];
+        p.m23 = H5 ? rr[3 * WAVE] : 0.f;
+        p.t11 = p.t12 = p.t21 = p.t22 = 0.f;
+        if constexpr (TB) {
+            p.t11 = rr[4 * WAVE];
+            p.t12 = rr[5 * WAVE];
+            p.t21 = rr[6 * WAVE];
+            p.t22 = rr[7 * WAVE];
+        }
+        return p;
+    };
+    Pre cur = pre_load(4);
     for (int s = 4; s <= s_end; s++) {
-        const int par = s & 1;
+        const int sl = s % 3;
+        const Pre nxt = pre_load(s + 1);
         const int umax = min(30, s - 6);   // no interior loop fits a span below 6
-        const int ncell = (s <= N - 1 && umax >= 0) ? uni(L.rcnt[par]) : 0;
+        const int ncell = (s <= N - 1 && umax >= 0) ? uni(cur.n) : 0;
         for (int c0 = 0; c0 < ncell; c0 += WAVE / 4) {
             const int idx = c0 + cq;   // the lane's cell (records: set idx / 64, lane idx % 64)
-            const float *rr = L.rec + ((par * 2 + (idx >> 6)) * PX_RF) * WAVE + (idx & (WAVE - 1));
             // word: i | ty << 7 | A << 10 | B << 18 | masked << 26 | real << 27; a block
             // reads only the fields its sizes use
-            const int fl = __float_as_int(rr[0]);
+            Pre q = cur;
+            if (c0 > 0) {
+                const float *rr = L.rec + ((sl * 2 + (idx >> 6)) * PX_RF) * WAVE + (idx & (WAVE - 1));
+                q.fl = __float_as_int(rr[0]);
+                q.mmo = rr[WAVE];
+                q.mo = rr[2 * WAVE];
+                q.m23 = H5 ? rr[3 * WAVE] : 0.f;
+                if constexpr (TB) {
+                    q.t11 = rr[4 * WAVE];
+                    q.t12 = rr[5 * WAVE];
+                    q.t21 = rr[6 * WAVE];
+                    q.t22 = rr[7 * WAVE];
+                }
+            }
+            const int fl = q.fl;
             PxCell c;
             c.i = fl & 127;
             const int ty = (fl >> 7) & 7;
             c.ty8 = ty * 8;
             c.A = (fl >> 10) & 255;
             c.B = (fl >> 18) & 255;
-            const float mmo = rr[WAVE];
+            const float mmo = q.mmo;
             c.tau = ty > 2 ? eTAU : 1.f;
-            c.mo = rr[2 * WAVE];
-            c.m23 = H5 ? rr[3 * WAVE] : 0.f;
-            c.t11 = c.t12 = c.t21 = c.t22 = 0.f;
-            if constexpr (TB) {
-                c.t11 = rr[4 * WAVE];
-                c.t12 = rr[5 * WAVE];
-                c.t21 = rr[6 * WAVE];
-                c.t22 = rr[7 * WAVE];
-            }
+            c.mo = q.mo;
+            c.m23 = q.m23;
+            c.t11 = q.t11;
+            c.t12 = q.t12;
+            c.t21 = q.t21;
+            c.t22 = q.t22;
             const float outer = r < 2 ? c.tau : c.mo;
             f2 g = {0.f, 0.f}, sp = {0.f, 0.f}, gs = {0.f, 0.f}, sps = {0.f, 0.f};
             PSTAMP(2);
@@ -398,8 +435,9 @@ __device__ __forceinline__ void pb_sweep(const PxL &L, const DevScaled *XS, int 
             // small sizes count once (phase 0), then the cell's total over its four lanes
             const f2 part = quad_sum(fma2(g, sp2(mmo), sp) + (r == 0 ? fma2(gs, sp2(mmo), sps) : f2{0.f, 0.f}));
             if (r == 0 && idx < ncell && ((fl >> 27) & 1))
-                L.part[((par * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] = part;
+                L.part[(((s & 1) * 2 + ((c.i - 1) >> 6)) * PX_NB + wid) * WAVE + ((c.i - 1) & (WAVE - 1))] = part;
         }
+        cur = nxt;
         PSTAMP(5);
         lds_barrier();
         PSTAMP(6);
@@ -428,7 +466,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     L.cc = reinterpret_cast<uint8_t *>(smem + Y.CC);
     L.part = reinterpret_cast<f2 *>(smem + Y.PART);
     L.rec = reinterpret_cast<float *>(smem + Y.REC);
-    L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(2) * 2 * PX_RF * WAVE * 4);
+    L.rcnt = reinterpret_cast<int *>(smem + Y.REC + size_t(3) * 2 * PX_RF * WAVE * 4);
     L.cl = reinterpret_cast<uint8_t *>(smem + Y.CL);       // cl[off(D) + rank] = i
     L.cn = L.cl + Y.C;                                      // cn[D] = count
     L.mla = reinterpret_cast<f2 *>(smem + Y.MLA);
@@ -763,7 +801,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (k * WAVE >= P.n) break;
-            float *r = L.rec + (((D & 1) * 2 + k) * PX_RF) * WAVE + lane;
+            float *r = L.rec + (((D % 3) * 2 + k) * PX_RF) * WAVE + lane;
             r[0] = __int_as_float(P.w1[k]);
             r[WAVE] = P.mmo[k];
             r[2 * WAVE] = P.mo[k];
@@ -773,16 +811,17 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             r[6 * WAVE] = P.t21[k];
             r[7 * WAVE] = P.t22[k];
         }
-        if (lane == 0) L.rcnt[D & 1] = P.n;
+        if (lane == 0) L.rcnt[D % 3] = P.n;
     };
     Pend pend;
     Seq seqp;
     Idx idxp;
-    if (wid == PX_WR) {
-        rec_store(4, rec_load(4, seq_load(4, idx_load(4))));   // the sweep's first B diagonal (no loop fits: count 0)
-        pend = rec_load(5, seq_load(5, idx_load(5)));
-        seqp = seq_load(6, idx_load(6));
-        idxp = idx_load(7);
+    if (wid == PX_WR) {   // the records run two steps ahead of B (which loads them one step ahead)
+        rec_store(4, rec_load(4, seq_load(4, idx_load(4))));   // the sweep's first B diagonals (no loop fits: count 0)
+        rec_store(5, rec_load(5, seq_load(5, idx_load(5))));
+        pend = rec_load(6, seq_load(6, idx_load(6)));
+        seqp = seq_load(7, idx_load(7));
+        idxp = idx_load(8);
     }
     __syncthreads();
 
@@ -938,12 +977,12 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 }
                 qfac(j + 1);
             } else if (wid == PX_WR) {
-                // ---------------- R: records of diagonal s + 1 (next step's B), tables of
-                // s + 2, bases of s + 3, rank list of s + 4
-                rec_store(s + 1, pend);
-                pend = rec_load(s + 2, seqp);
-                seqp = seq_load(s + 3, idxp);
-                idxp = idx_load(s + 4);
+                // ---------------- R: records of diagonal s + 2 (B loads them next step for
+                // the step after), tables of s + 3, bases of s + 4, rank list of s + 5
+                rec_store(s + 2, pend);
+                pend = rec_load(s + 3, seqp);
+                seqp = seq_load(s + 4, idxp);
+                idxp = idx_load(s + 5);
             }
             PSTAMP(4);
             lds_barrier();
