@@ -214,6 +214,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         (L.cc - (NM - 3))[k] = 0;
     }
 
+#ifdef ADX_STAMP
+    const unsigned long long st_s1 = __builtin_amdgcn_s_memtime();   // restore issued, setup tables
+#endif
     // ---- sequence, constraint arrays, motif sites (mfe_cells.hip)
     const uint8_t *cons = ka.cons + V.cons_off;
     const int np = N + 2;
@@ -253,11 +256,28 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         L.S[N + 1] = L.S[1];
     }
     const int mL = XS->motif_len;
+#ifdef ADX_STAMP
+    const unsigned long long st_s2 = __builtin_amdgcn_s_memtime();   // sequence, constraints
+#endif
     if ((mh0 || mh1) && mL > 0) {
-        for (int o = tid + 1; o + mL - 1 <= N; o += NT) {
-            bool ok = true;
-            for (int k = 0; k < mL && ok; k++) ok = L.S[o + k] == mcode[k];
-            L.mat[o] = ok ? 1 : 0;
+        // lanes = starts; the motif's positions in chunks of 8 independent reads (one
+        // LDS round trip per chunk, not one per position of the longest match)
+        for (int o0 = 1 + wid * WAVE; o0 + mL - 1 <= N; o0 += NT) {
+            const int o = o0 + lane;
+            const bool in = o + mL - 1 <= N;
+            bool ok = in;
+            for (int k0 = 0; k0 < mL; k0 += 8) {
+                uint32_t sb[8], mb[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    sb[t] = L.S[min(o + k0 + t, N + 1)];
+                    mb[t] = mcode[k0 + t];
+                }
+#pragma unroll
+                for (int t = 0; t < 8; t++) ok = ok && (k0 + t >= mL || sb[t] == mb[t]);
+                if (__ballot(ok) == 0) break;
+            }
+            if (in) L.mat[o] = ok ? 1 : 0;
         }
         __syncthreads();
         for (int o = 1 + wid; o + mL - 1 <= N; o += NT / WAVE) {
@@ -282,6 +302,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         L.q5[0] = 0u;
         for (int j = 1; j <= 4 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] : INF16;
     }
+#ifdef ADX_STAMP
+    const unsigned long long st_s3 = __builtin_amdgcn_s_memtime();   // motif sites
+#endif
     // ---- per-cell setup (mfe_cells.hip): inner-pair code, hairpin (+ motif) or the
     // non-pairable mark, multiloop stem of the pairable cells
     for (int dd = 4 + wid; dd <= N - 1; dd += NWV) {
@@ -319,6 +342,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         }
     }
     __syncthreads();
+#ifdef ADX_STAMP
+    const unsigned long long st_s4 = __builtin_amdgcn_s_memtime();   // per-cell pass
+#endif
     // the partial, split and U slots start impossible (the setup used their space)
     for (int k = tid; k < 4 * 2 * NP; k += NT) L.part[k] = PINF;
     for (int k = tid; k < 6 * NP; k += NT) L.mla[k] = INF16;
@@ -413,6 +439,10 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     unsigned long long st_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
     st_acc[8] = st_last - st_setup0;
+    st_acc[11] = st_s1 - st_setup0;
+    st_acc[12] = st_s2 - st_s1;
+    st_acc[13] = st_s3 - st_s2;
+    st_acc[14] = st_s4 - st_s3;
 #endif
     int sl = 0;   // list slot of this step: step index % 3
     for (int d = 6; d - 3 <= N; d += 2) {
