@@ -443,7 +443,8 @@ struct Problem {
                                  //   and the pair-term score that waits for the outside pass)
     DevBuf<uint8_t> dCur, dValid;
     DevBuf<int> dChg;
-    DevBuf<int> dOrder;          // launch order of the MC step's folds (KArgs::order)
+    DevBuf<int> dOrder;          // launch order of a rescore's folds (KArgs::order, order_kernel)
+    DevBuf<uint8_t> dCls;        // the folds' weight classes (KArgs::ocls, the proposals' or a rescore's)
     size_t tab_slot = 0;
     bool state_on = false;   // set for MC launches only (not for adx_score_batch)
     std::unique_ptr<DevTables> hT;
@@ -470,7 +471,7 @@ struct Problem {
     }
 
     KArgs kargs() const {
-        KArgs ka;
+        KArgs ka{};
         ka.T = dT.p;
         ka.X = dX.p;
         ka.variants = dV.p;
@@ -506,6 +507,7 @@ struct Problem {
         ka.tab_valid = st ? dValid.p : nullptr;
         ka.chg = st ? dChg.p : nullptr;
         ka.order = st && !std::getenv("ADX_NO_ORDER") ? dOrder.p : nullptr;
+        ka.ocls = dCls.p;
         ka.gstep = dGstep.p;
         ka.pf_ring = pf_ring ? 1 : 0;
         ka.ring_scratch = dRingScr.p;
@@ -585,6 +587,7 @@ struct Problem {
         HIP_TRY(dValid.alloc(W));
         HIP_TRY(dChg.alloc(size_t(W) * 2));
         HIP_TRY(dOrder.alloc(W));
+        HIP_TRY(dCls.alloc(W));
         if (adx_status sg = ensure_gstep(W)) return sg;
         HIP_TRY(hipMemsetAsync(dCur.p, 1, W, stream));     // the initial fold writes slot 0
         HIP_TRY(hipMemsetAsync(dValid.p, 0, W, stream));

@@ -186,10 +186,16 @@ struct KArgs {
     // waits for the outside pass (pair terms): score_kernel -> bppm_kernel
     // (re-using the inside tables just written) -> combine_kernel
     float *gstep;
-    // MC steps: the walkers in launch order, heaviest refold first (kernels.hip
-    // order_kernel; mfe_cells_kernel / pf_cells_kernel map blockIdx through it
-    // so the long folds do not trail the launch); null: blockIdx order
-    const int *order;
+    // MC steps: the walkers in launch order, heaviest refold first, so the long
+    // folds do not trail the launch (kernels.hip order_kernel, from the weight
+    // classes in ocls); the fold kernels map blockIdx through it
+    // (fold_common.hpp walker_at); null: blockIdx order
+    int *order;
+    const uint8_t *ocls;
+    // MC steps: the scores a fold launch leaves as per-variant energies in gstep
+    // are combined by the step's tail (kernels.hip accept_walker), not by a
+    // combine_kernel launch of their own
+    int defer_comb;
 };
 
 // Monte Carlo state (device, read/write).
@@ -230,6 +236,12 @@ struct StepArgs {
     double *tr_temp, *tr_prop, *tr_cur, *tr_u;
     double *tr_terms;           // [(s*W + w) * n_terms_total]
     int *chg;                   // W * 2: hull of the positions the proposal changed (-1: none)
+    // the weight class of the proposal's fold (KArgs::ocls; null: none), the
+    // incremental-fold state accept updates and the MFE overflow flags a
+    // proposal clears (null when absent)
+    uint8_t *cls;
+    uint8_t *cur_slot, *tab_valid;
+    int *ovf;
 };
 
 }  // namespace adx

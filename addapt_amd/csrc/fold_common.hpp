@@ -27,6 +27,15 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The walker a fold workgroup takes at launch position wb (order: a step's
+// launch order, kernels.hip order_kernel; null: blockIdx order), or -1 when
+// mask (1 = fold) leaves it nothing to fold.
+__device__ __forceinline__ int walker_at(const int *order, const int *mask, int wb) {
+    const int w = order ? order[wb] : wb;
+    if (mask && mask[w] != 1) return -1;
+    return w;
+}
+
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 constexpr int MFE16_FLOOR = -12000;
 

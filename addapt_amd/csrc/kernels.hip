@@ -1239,6 +1239,40 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
     return s;
 }
 
+// combine_score's arithmetic (scoring.cc:53-71): term idx (= context * n_terms
+// + term) of the walker whose per-variant energies are g and pair
+// probabilities pp (null: the pair terms read 0.5)
+__device__ __forceinline__ double term_value(const KArgs &ka, const float *g, const double *pp, int idx,
+                                             double &weight) {
+    const DevTermMap m = ka.tmap[idx];
+    double p = (m.kind == 1) ? (pp ? pp[m.pidx] : 0.5)
+                             : exp((static_cast<double>(g[m.vfree]) - static_cast<double>(g[m.vcons])) / ka.X->kT);
+    if (!m.favorable) p = 1.0 - p;
+    weight = m.weight;
+    return log(p);
+}
+
+// The score of walker w from KArgs::gstep, one wave: the terms' values on
+// lanes, summed in term order (the same sum as combine_kernel's loop); tv
+// (the walker's term values, optional).  Result uniform.
+__device__ double combine_wave(const KArgs &ka, int w, int lane, double *tv) {
+    const float *g = ka.gstep + size_t(w) * ka.n_variants;
+    const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
+    const int nt = ka.n_terms * ka.n_ctx_eff;
+    double score = 0.0;
+    for (int b0 = 0; b0 < nt; b0 += WAVE) {
+        const int idx = b0 + lane;
+        double val = 0.0, wt = 0.0;
+        if (idx < nt) {
+            val = term_value(ka, g, pp, idx, wt);
+            if (tv) tv[idx] = val;
+        }
+        const int n = min(WAVE, nt - b0);
+        for (int k = 0; k < n; k++) score += __shfl(wt, k, WAVE) * __shfl(val, k, WAVE);
+    }
+    return score;
+}
+
 template <int NT, int P, class SR>
 __global__ void __launch_bounds__(NT, (NT >= 1024) ? 4 : (NT > 512) ? 3 : (P == 2 ? 2 : 4))   // min waves per SIMD
 score_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, double *scores,
@@ -1705,19 +1739,29 @@ __device__ void mt_twist_wave(uint32_t *mt, int lane) {
     }
 }
 
+// A walker's MT19937 stream (MT_WORDS words in HBM: state + index) as a step
+// reads it: only the words [lo, hi) it will draw are staged in LDS (a step
+// draws a few), the whole state only when it twists (then written back).
 struct MtView {
-    uint32_t *mt;
-    int idx;
+    uint32_t *mt;          // LDS, words [lo, hi) valid
+    const uint32_t *g;     // HBM state
+    int idx, lo, hi;
     bool twisted;
 };
 
 __device__ uint32_t mt_next(MtView &g, int lane) {
     if (g.idx >= 624) {
+        if (g.lo != 0 || g.hi != 624) {
+            for (int k = lane; k < 624; k += WAVE) g.mt[k] = g.g[k];
+            __syncthreads();
+            g.lo = 0;
+            g.hi = 624;
+        }
         mt_twist_wave(g.mt, lane);
         g.idx = 0;
         g.twisted = true;
     }
-    uint32_t y = g.mt[g.idx];
+    uint32_t y = (g.idx < g.hi) ? g.mt[g.idx] : g.g[g.idx];   // past the window: a rejection draw
     g.idx++;
     y ^= y >> 11;
     y ^= (y << 7) & 0x9d2c5680u;
@@ -1847,21 +1891,104 @@ __device__ void nth_element_libstdcxx(double *a, int k, int n) {
 }
 
 // ---------------------------------------------------------------- MC step
-// One MonteCarlo::apply iteration (sampling.cc:55-99) = three launches on one
-// stream: propose_kernel (thermostat, RNG streams, mutation move, unchanged
-// check; one wave per walker) -> score_kernel masked to the walkers whose
-// sequence changed -> accept_kernel (Metropolis, one wave per walker).
-// Splitting keeps the fold kernel's register allocation free of the MC state.
-__global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step, int s) {
-    const int w = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (w >= st.W) return;
+// One MonteCarlo::apply iteration (sampling.cc:55-99) on one stream: the fold
+// launches of the walkers whose sequence changed (launch_window) between two
+// runs of step_tail_kernel, one wave per walker: the Metropolis decision of
+// the step before (accept_walker) and the next proposal (propose_walker:
+// thermostat, RNG streams, mutation move, unchanged check) with its fold's
+// weight class (fold_class, for order_kernel).  The MC state stays out of the
+// fold kernels' register allocation.
+
+struct Accepted {
+    bool ran = false;       // a decision was taken (no move error)
+    bool changed = false;   // the proposal was scored: last_diff = diff
+    bool took = false;      // accepted: the proposal is the current sequence
+    double diff = 0.0;
+    int tab_valid = -1;     // >= 0: the walker's new tab_valid
+};
+
+// Metropolis (sampling.cc:76-89).  cur_slot / tab_valid (null without stored
+// tables): an accepted proposal's tables become current, and complete (every
+// kernel writes the whole slot), so a walker whose current tables were invalid
+// (imported configuration, MFE fold outside the 16-bit range) refolds
+// incrementally again -- unless this very fold left the 16-bit range (ovf,
+// MFE: its slot is not exact).  Every lane takes the (uniform) decision, lane 0
+// writes the walker's state, and an accepted proposal's sequence is copied by
+// the whole wave (coalesced).
+// kc (comb set): the step's fold launches left the proposal's score as
+// per-variant energies (KArgs::defer_comb): combined here (combine_wave) and
+// stored, but for an MFE fold the FP32 fallback redid (ovf; it stored the score).
+__device__ Accepted accept_walker(const StepArgs &st, const KArgs &kc, bool comb, double *tv, int w, int lane, int s,
+                                  int nt_tot) {
+    Accepted a;
+    if (st.err[w]) return a;
+    a.ran = true;
+    const bool changed = st.changed[w] == 1;
+    int outcome = 2;  // ACCEPT_UNCHANGED
+    double prop;
+    if (changed && comb && !(st.ovf && st.ovf[w])) {
+        prop = combine_wave(kc, w, lane, tv ? tv + size_t(w) * nt_tot : nullptr);
+        if (lane == 0) st.prop_score[w] = prop;
+    } else {
+        prop = st.prop_score[w];
+    }
+    double diff = 0.0;
+    if (changed) {
+        diff = prop - st.cur_score[w];
+        const double crit = exp(diff / st.temp[w]);
+        outcome = (crit < st.u[w]) ? 0 : (diff > 0) ? 3 : 1;
+    }
+    a.changed = changed;
+    a.diff = diff;
+    const bool acc = outcome == 1 || outcome == 3;
+    a.took = acc;
+    if (acc) {
+        const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
+        uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
+        for (int k = lane; k < st.Nraw; k += WAVE) c[k] = p[k];
+        if (st.cur_slot) a.tab_valid = (st.ovf && st.ovf[w]) ? 0 : 1;
+    }
+    if (lane == 0) {
+        if (changed) st.last_diff[w] = diff;
+        if (acc) {
+            st.cur_score[w] = prop;
+            if (st.cur_slot) {
+                st.cur_slot[w] ^= 1;   // the proposal's tables become current
+                st.tab_valid[w] = uint8_t(a.tab_valid);
+            }
+        }
+        st.counters[size_t(w) * 4 + outcome] += 1;
+        if (st.tr_pos) {
+            const size_t r = size_t(s) * st.W + w;
+            st.tr_outcome[r] = outcome;
+            st.tr_prop[r] = changed ? prop : __builtin_nan("");
+            st.tr_cur[r] = acc ? prop : st.cur_score[w];
+            st.tr_u[r] = changed ? st.u[w] : __builtin_nan("");
+            if (!changed && st.tr_terms)
+                for (int k = 0; k < nt_tot; k++) st.tr_terms[r * nt_tot + k] = __builtin_nan("");
+        }
+    }
+    return a;
+}
+
+struct Proposed {
+    bool scored = false;    // the fold launch scores this walker
+    int plo = -1, phi = -1;
+};
+
+// The proposal of step `step` (trace row s).  acc: the decision this wave just
+// took -- an accepted proposal is read where it is (prop_seq) rather than from
+// the copy the wave just wrote, and the score difference is the auto
+// thermostat's training value.  mt: 2 * MT_WORDS words of LDS.
+__device__ Proposed propose_walker(const StepArgs &st, long long step, int s, int w, int lane, const Accepted &acc,
+                                   uint32_t *mt) {
+    Proposed out;
     if (st.err[w]) {
         if (lane == 0) st.changed[w] = 0;
-        return;
+        return out;
     }
-    __shared__ uint32_t mt[2 * MT_WORDS];
-    uint8_t *cur = st.cur_seq + size_t(w) * st.Nraw;
+    uint8_t *prop = st.prop_seq + size_t(w) * st.Nraw;
+    const uint8_t *cur = acc.took ? prop : st.cur_seq + size_t(w) * st.Nraw;
     uint32_t *gA = st.mtA + size_t(w) * MT_WORDS;
     uint32_t *gC = st.mtC + size_t(w) * MT_WORDS;
     // ---- thermostat (sampling.cc:59; 309-401)
@@ -1877,7 +2004,7 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
         T = st.auto_T[w];
         double Tn = T;
         if (lane == 0) {
-            tr[n - 1] = st.last_diff[w];
+            tr[n - 1] = acc.changed ? acc.diff : st.last_diff[w];
             if (n >= st.period) {
                 // median = std::nth_element at n/2, clamp = std::max(t, 0.0)
                 // (sampling.cc:389-396): the libstdc++ selection, so -0.0 / NaN
@@ -1894,14 +2021,17 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
         }
         T = __shfl(Tn, 0, WAVE);
     }
-    // ---- move: stream A (and C if the step will be scored)
+    // ---- move: stream A (and C if the step will be scored); the next 8 words of
+    // each stream staged (a step draws 2 + 2 but for a rejection)
     uint32_t *mA = mt, *mC = mt + MT_WORDS;
-    for (int k = lane; k < 624; k += WAVE) {
-        mA[k] = gA[k];
-        mC[k] = gC[k];
+    const int ia = int(gA[624]), ic = int(gC[624]);
+    if (lane < 8) {
+        if (ia + lane < 624) mA[ia + lane] = gA[ia + lane];
+    } else if (lane < 16) {
+        if (ic + lane - 8 < 624) mC[ic + lane - 8] = gC[ic + lane - 8];
     }
     __syncthreads();
-    MtView a{mA, int(gA[624]), false}, c{mC, int(gC[624]), false};
+    MtView a{mA, gA, ia, ia, min(ia + 8, 624), false}, c{mC, gC, ic, ic, min(ic + 8, 624), false};
     const int pick = int(mt_uniform(a, uint32_t(st.M), lane));
     const int bcode = int(mt_uniform(a, 4u, lane)) + 1;  // "ACGU"[r]
     const int e = st.clo_err[pick];
@@ -1926,13 +2056,13 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
     }
     double u = 0.0;
     if (e == 0 && changed) u = mt_canonical(c, lane);
-    for (int k = lane; k < 624; k += WAVE) {
-        if (a.twisted) gA[k] = mA[k];
-        if (c.twisted) gC[k] = mC[k];
-    }
+    if (a.twisted)
+        for (int k = lane; k < 624; k += WAVE) gA[k] = mA[k];
+    if (c.twisted)
+        for (int k = lane; k < 624; k += WAVE) gC[k] = mC[k];
     if (changed) {
-        uint8_t *prop = st.prop_seq + size_t(w) * st.Nraw;
-        for (int k = lane; k < st.Nraw; k += WAVE) prop[k] = cur[k];
+        if (!acc.took)
+            for (int k = lane; k < st.Nraw; k += WAVE) prop[k] = cur[k];
         __syncthreads();
         for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE)
             prop[st.clo_pos[k]] = uint8_t(st.clo_par[k] ? 5 - bcode : bcode);
@@ -1957,53 +2087,43 @@ __global__ void __launch_bounds__(64) propose_kernel(StepArgs st, long long step
             st.tr_temp[r] = T;
         }
     }
+    out.scored = e == 0 && changed;
+    out.plo = changed ? plo : -1;
+    out.phi = changed ? phi : -1;
+    return out;
 }
 
-// cur_slot / tab_valid (null without stored tables): an accepted proposal's
-// tables become current, and complete (every kernel writes the whole slot),
-// so a walker whose current tables were invalid (imported configuration,
-// MFE fold outside the 16-bit range) refolds incrementally again -- unless
-// this very fold left the 16-bit range (ovf, MFE: its slot is not exact)
-// One wave per walker (4 walkers per 256-thread block): every lane takes the
-// (uniform) Metropolis decision, lane 0 writes the walker's state, and an
-// accepted proposal's sequence is copied by the whole wave (coalesced).
-__global__ void __launch_bounds__(256) accept_kernel(StepArgs st, int s, int nt_tot, uint8_t *cur_slot,
-                                                     uint8_t *tab_valid, const int *ovf) {
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & (WAVE - 1);
-    if (w >= st.W || st.err[w]) return;
-    const bool changed = st.changed[w] == 1;
-    int outcome = 2;  // ACCEPT_UNCHANGED
-    const double prop = st.prop_score[w];
-    double diff = 0.0;
-    if (changed) {
-        diff = prop - st.cur_score[w];
-        const double crit = exp(diff / st.temp[w]);
-        outcome = (crit < st.u[w]) ? 0 : (diff > 0) ? 3 : 1;
-    }
-    if (outcome == 1 || outcome == 3) {
-        const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
-        uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
-        for (int k = lane; k < st.Nraw; k += WAVE) c[k] = p[k];
-    }
-    if (lane != 0) return;
-    if (changed) st.last_diff[w] = diff;
-    if (outcome == 1 || outcome == 3) {
-        st.cur_score[w] = prop;
-        if (cur_slot) {
-            cur_slot[w] ^= 1;   // the proposal's tables become current
-            tab_valid[w] = (ovf && ovf[w]) ? 0 : 1;
+// The weight class of a proposal's fold for the launch order (order_kernel):
+// 0 = heaviest .. 63 by the band of cells containing a changed position, about
+// (m_hi + 2) (N - m_lo + 1), a fold from scratch (no valid stored tables)
+// counting as the whole triangle; 64 = not scored.
+__device__ __forceinline__ int fold_class(const StepArgs &st, const Proposed &p, int tabv) {
+    if (!p.scored) return 64;
+    const long long full = (long long)st.Nraw * st.Nraw;
+    long long key = full;
+    if (tabv && st.chg && p.plo >= 0) key = (long long)(p.phi + 2) * (st.Nraw - p.plo + 1);
+    return 63 - int(min(full, max(0LL, key)) * 63 / (full > 0 ? full : 1));
+}
+
+// One wave per walker: the decision of step s_acc (< 0: none, the first
+// proposal of a launch; comb, tv: accept_walker) and the proposal of global step `step` (< 0: none, the
+// last step of a launch; trace row s_prop).  Across a launch_steps call the
+// two halves of a step meet only through HBM written by the launches between.
+__global__ void __launch_bounds__(64) step_tail_kernel(StepArgs st, KArgs kc, int comb, double *tv, int s_acc,
+                                                        long long step, int s_prop, int nt_tot) {
+    __shared__ uint32_t mt[2 * MT_WORDS];
+    const int w = blockIdx.x;
+    const int lane = threadIdx.x;
+    Accepted acc;
+    if (s_acc >= 0) acc = accept_walker(st, kc, comb != 0, tv, w, lane, s_acc, nt_tot);
+    if (step < 0) return;
+    const Proposed p = propose_walker(st, step, s_prop, w, lane, acc, mt);
+    if (lane == 0) {
+        if (st.ovf) st.ovf[w] = 0;   // set again by this proposal's fold if it leaves the 16-bit range
+        if (st.cls) {
+            const int tabv = !st.tab_valid ? 0 : acc.tab_valid >= 0 ? acc.tab_valid : st.tab_valid[w];
+            st.cls[w] = uint8_t(fold_class(st, p, tabv));
         }
-    }
-    st.counters[size_t(w) * 4 + outcome] += 1;
-    if (st.tr_pos) {
-        const size_t r = size_t(s) * st.W + w;
-        st.tr_outcome[r] = outcome;
-        st.tr_prop[r] = changed ? prop : __builtin_nan("");
-        st.tr_cur[r] = st.cur_score[w];
-        st.tr_u[r] = changed ? st.u[w] : __builtin_nan("");
-        if (!changed && st.tr_terms)
-            for (int k = 0; k < nt_tot; k++) st.tr_terms[r * nt_tot + k] = __builtin_nan("");
     }
 }
 
@@ -2083,18 +2203,12 @@ __global__ void combine_kernel(KArgs ka, int W, const int *mask, double *scores,
     const double *pp = ka.pair_p ? ka.pair_p + size_t(w) * ka.n_pairs : nullptr;
     const int nt = ka.n_terms * ka.n_ctx_eff;
     double *tv = terms ? terms + size_t(w) * nt : nullptr;
-    const DevScaled &X = *ka.X;
     double score = 0.0;
-    for (int c = 0; c < ka.n_ctx_eff; c++) {
-        for (int t = 0; t < ka.n_terms; t++) {
-            const DevTermMap m = ka.tmap[c * ka.n_terms + t];
-            double p = (m.kind == 1) ? (pp ? pp[m.pidx] : 0.5)
-                                     : exp((static_cast<double>(g[m.vfree]) - static_cast<double>(g[m.vcons])) / X.kT);
-            if (!m.favorable) p = 1.0 - p;
-            const double val = log(p);
-            if (tv) tv[c * ka.n_terms + t] = val;
-            score += m.weight * val;
-        }
+    for (int idx = 0; idx < nt; idx++) {
+        double wt;
+        const double val = term_value(ka, g, pp, idx, wt);
+        if (tv) tv[idx] = val;
+        score += wt * val;
     }
     scores[w] = score;
 }
@@ -2181,11 +2295,13 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
             // scratch), then the scores (the same arithmetic as combine_score)
             if (!g) return hipErrorInvalidValue;
             e = launch_mfe_cells(k16, seqs, W, g, mask, stream);
-            if (e != hipSuccess) return e;
-            KArgs kc = ka;
-            kc.gstep = g;
-            hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
-            e = hipGetLastError();
+            if (e == hipSuccess && !(ka.defer_comb && mask)) {
+                KArgs kc = ka;
+                kc.gstep = g;
+                hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores,
+                                   terms);
+                e = hipGetLastError();
+            }
         } else {
             e = launch_score_t<ADX_NT16, 1, MinPlus16>(k16, seqs, W, scores, terms, dG, mask, stream);
         }
@@ -2209,6 +2325,7 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
             // lanes = cells (pf_cells.hip): energies to dG (or the gstep scratch), then the scores
             hipError_t e = launch_pf_cells(ka, seqs, W, mask, g, stream);
             if (e != hipSuccess) return e;
+            if (ka.defer_comb && mask) return hipSuccess;   // the step's tail combines
             KArgs kc = ka;
             kc.gstep = g;
             hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
@@ -2219,6 +2336,7 @@ hipError_t launch_score_m(const KArgs &ka, const uint8_t *seqs, int W, double *s
             if (!g) return hipErrorInvalidValue;
             hipError_t e = launch_pf_ring(ka, seqs, W, mask, g, ka.tab ? nullptr : ka.ring_scratch, stream);
             if (e != hipSuccess) return e;
+            if (ka.defer_comb && mask) return hipSuccess;   // the step's tail combines
             KArgs kc = ka;
             kc.gstep = g;
             hipLaunchKernelGGL(combine_kernel, dim3((W + 255) / 256), dim3(256), 0, stream, kc, W, mask, scores, terms);
@@ -2316,43 +2434,46 @@ hipError_t launch_bppm(const KArgs &ka, const uint8_t *seqs, int W, const int *m
     return launch_bppm_r(ka, seqs, W, mask, full, ld, pair_p, scratch, stream, false);
 }
 
-// Launch order of an MC step's folds: walkers whose proposal is scored, the
-// heaviest refold first (the band of cells containing a changed position,
-// about (m_hi + 2) (N - m_lo + 1); a fold from scratch counts as the whole
-// triangle), then the unscored ones (their blocks exit at once).  The folds'
-// durations vary by several times and the GPU starts workgroups in launch
-// order, so heavy folds no longer trail the launch.  64 weight classes, one
-// workgroup, LDS counters; the order within a class does not matter (each
-// walker's fold is independent of where it runs).
-__global__ void __launch_bounds__(1024) order_kernel(int W, const int *changed, const int *chg,
-                                                     const uint8_t *tab_valid, int Nraw, int *order, int *ovf) {
-    constexpr int NB = 65;   // 64 weight classes (0 = heaviest) + the unscored walkers
-    __shared__ int hist[NB], base[NB];
-    for (int k = threadIdx.x; k < NB; k += blockDim.x) hist[k] = 0;
+// Launch order of an MC step's folds: the walkers whose proposal is scored,
+// heaviest refold first, then the unscored ones (their blocks exit at once) --
+// a counting sort of the weight classes the proposals computed (fold_class;
+// a rescore's are all 0).  The folds' durations vary by several times and the
+// GPU starts workgroups in launch order, so heavy folds no longer trail the
+// launch.  One workgroup, LDS counters, the class bases by one wave's scan;
+// the order within a class does not matter (each walker's fold is independent
+// of where it runs).
+__global__ void __launch_bounds__(1024) order_kernel(int W, const uint8_t *cls, int *order) {
+    __shared__ int hist[65];
+    const int tid = threadIdx.x;
+    if (tid < 65) hist[tid] = 0;
     __syncthreads();
-    const long long full = (long long)Nraw * Nraw;
-    auto bin_of = [&](int w) -> int {
-        if (changed[w] != 1) return NB - 1;
-        long long key = full;
-        if (tab_valid && tab_valid[w] && chg && chg[2 * w] >= 0)
-            key = (long long)(chg[2 * w + 1] + 2) * (Nraw - chg[2 * w] + 1);
-        const int b = int(min(full, max(0LL, key)) * 63 / (full > 0 ? full : 1));
-        return 63 - b;
-    };
-    for (int w = threadIdx.x; w < W; w += blockDim.x) {
-        atomicAdd(&hist[bin_of(w)], 1);
-        if (ovf) ovf[w] = 0;   // the 16-bit MFE folds' overflow flags (launch_mfe_cells skips its memset)
-    }
+#pragma unroll 4
+    for (int w = tid; w < W; w += 1024) atomicAdd(&hist[cls[w]], 1);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int k = 0; k < NB; k++) {
-            base[k] = acc;
-            acc += hist[k];
+    if (tid < WAVE) {   // exclusive scan of classes 0..63; the unscored (64) after them
+        const int h = hist[tid];
+        int incl = h;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int t = __shfl_up(incl, o, WAVE);
+            if (tid >= o) incl += t;
         }
+        hist[tid] = incl - h;
+        if (tid == WAVE - 1) hist[64] = incl;
     }
     __syncthreads();
-    for (int w = threadIdx.x; w < W; w += blockDim.x) order[atomicAdd(&base[bin_of(w)], 1)] = w;
+#pragma unroll 4
+    for (int w = tid; w < W; w += 1024) order[atomicAdd(&hist[cls[w]], 1)] = w;
+}
+
+// Whether launch_window leaves a step's scores as energies in gstep (KArgs::
+// defer_comb set): the fold kernels that write per-variant energies and the
+// outside pass of the pair terms
+static bool window_defers(const KArgs &ka) {
+    if (!ka.defer_comb) return false;
+    if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) return true;
+    const InsideK k = inside_choice(ka, ka.gstep != nullptr);
+    return k == InsideK::MfeCells || k == InsideK::PfCells || k == InsideK::PfRing;
 }
 
 // The score window of one MC step for the walkers flagged in `changed`: the
@@ -2363,9 +2484,7 @@ __global__ void __launch_bounds__(1024) order_kernel(int W, const int *changed, 
 static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *changed, double *tv,
                                 hipStream_t stream, hipEvent_t *evs) {
     if (evs) (void)hipEventRecord(evs[0], stream);
-    if (ka.order)
-        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, st.W, changed, ka.chg, ka.tab_valid, ka.Nraw,
-                           const_cast<int *>(ka.order), ka.mode == 1 ? ka.ovf : nullptr);
+    if (ka.order) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, st.W, ka.ocls, ka.order);
     hipError_t e;
     if (ka.n_pairs > 0 && ka.mode == 0 && ka.tab && ka.gstep) {
         // inside folds first (they write the proposal's tables), then the outside
@@ -2386,9 +2505,11 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
                                 ka.bppm_scratch, stream, true);
         if (e != hipSuccess) return e;
         if (evs) (void)hipEventRecord(evs[2], stream);
-        hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, changed,
-                           st.prop_score, tv);
-        e = hipGetLastError();
+        if (!ka.defer_comb) {
+            hipLaunchKernelGGL(combine_kernel, dim3((st.W + 255) / 256), dim3(256), 0, stream, ka, st.W, changed,
+                               st.prop_score, tv);
+            e = hipGetLastError();
+        }
     } else {
         // events 1 / 2 bracket the outside pass (here before the folds; none: empty)
         if (evs) (void)hipEventRecord(evs[1], stream);
@@ -2406,26 +2527,39 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
 
 // evs (optional): 4 * nsteps events per step: window start, outside pass
 // start, outside pass end, window end (score written); the inside share of a
-// window is the window minus its outside pass (adx_api.cpp)
-hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st, hipStream_t stream, hipEvent_t *evs) {
+// window is the window minus its outside pass (adx_api.cpp).  Launches:
+// step_tail_kernel (the first proposals), then per step the score window and
+// step_tail_kernel (its decisions and the next step's proposals).
+hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st0, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
+    StepArgs st = st0;
+    st.cur_slot = ka.tab ? ka.cur_slot : nullptr;
+    st.tab_valid = ka.tab ? ka.tab_valid : nullptr;
+    st.ovf = ka.mode == 1 ? ka.ovf : nullptr;
+    st.cls = ka.order ? const_cast<uint8_t *>(ka.ocls) : nullptr;   // ordering off: ADX_NO_ORDER / no stored tables
+    hipLaunchKernelGGL(step_tail_kernel, dim3(st.W), dim3(64), 0, stream, st, ka, 0, (double *)nullptr, -1, st.step0,
+                       0, nt_tot);
+    KArgs kas = ka;
+    kas.defer_comb = 1;   // the tails combine the scores the windows leave as energies
+    const int comb = window_defers(kas) ? 1 : 0;
     for (int s = 0; s < st.nsteps; s++) {
-        hipLaunchKernelGGL(propose_kernel, dim3(st.W), dim3(64), 0, stream, st, st.step0 + s, s);
         double *tv = st.tr_terms ? st.tr_terms + size_t(s) * st.W * nt_tot : nullptr;
-        hipError_t e = launch_window(ka, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
+        hipError_t e = launch_window(kas, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(accept_kernel, dim3((st.W + 3) / 4), dim3(256), 0, stream, st, s, nt_tot,
-                           ka.tab ? ka.cur_slot : nullptr, ka.tab ? ka.tab_valid : nullptr,
-                           ka.mode == 1 ? ka.ovf : nullptr);
+        const bool more = s + 1 < st.nsteps;
+        hipLaunchKernelGGL(step_tail_kernel, dim3(st.W), dim3(64), 0, stream, st, kas, comb, tv, s,
+                           more ? st.step0 + s + 1 : -1LL, s + 1, nt_tot);
     }
     return hipGetLastError();
 }
 
-__global__ void rescore_begin_kernel(int W, int *changed, uint8_t *tab_valid) {
+__global__ void rescore_begin_kernel(int W, int *changed, uint8_t *tab_valid, uint8_t *cls, int *ovf) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     changed[w] = 1;
     if (tab_valid) tab_valid[w] = 0;
+    if (cls) cls[w] = 0;   // folds from scratch: one weight class
+    if (ovf) ovf[w] = 0;
 }
 
 __global__ void rescore_end_kernel(int W, uint8_t *cur_slot, uint8_t *tab_valid, const int *ovf) {
@@ -2447,7 +2581,8 @@ hipError_t launch_rescore(const KArgs &ka, const StepArgs &st, double *tv, hipSt
     hipError_t e = hipMemcpyAsync(st.prop_seq, st.cur_seq, size_t(st.W) * st.Nraw, hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) return e;
     const dim3 g((st.W + 255) / 256), b(256);
-    hipLaunchKernelGGL(rescore_begin_kernel, g, b, 0, stream, st.W, st.changed, ka.tab ? ka.tab_valid : nullptr);
+    hipLaunchKernelGGL(rescore_begin_kernel, g, b, 0, stream, st.W, st.changed, ka.tab ? ka.tab_valid : nullptr,
+                       ka.order ? const_cast<uint8_t *>(ka.ocls) : nullptr, ka.mode == 1 ? ka.ovf : nullptr);
     e = launch_window(ka, st, st.changed, tv, stream, nullptr);
     if (e != hipSuccess) return e;
     if (ka.tab)

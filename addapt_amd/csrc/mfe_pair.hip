@@ -917,8 +917,8 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     const int ng = ka.n_groups2;
     const int wb = int(blockIdx.x) / ng, g = int(blockIdx.x) % ng;
     if (wb >= W) return;
-    const int w = ka.order ? ka.order[wb] : wb;
-    if (mask && mask[w] != 1) return;
+    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
+    if (w < 0) return;
     {
         const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
         for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = gct[k];

@@ -513,18 +513,16 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         L.ow[wo] = uint8_t((tp >> 8) & 255);
     };
     // one part of a multiloop-sum item of diagonal d (massign): qmb or r2 of
-    // lane-set ls, split points pi / np of the lane-set's longest range.  The
-    // slot terms are read in straight-line chunks of MC global loads issued
-    // together and then consumed (one L2 round trip per chunk: a pipeline of
-    // small batches across loop iterations left the compiler waiting on each
-    // load, vmcnt(0..7))
+    // lane-set ls, split points pi / np of the lane-set's longest range
     auto mpart = [&](int d, bool isq, int ls, int pi, int np) {
         int i = 1 + ls * WAVE + lane;
         const int ilast = min(N - d, (ls + 1) * WAVE);
         if (i > N - d) i = N - d;
         const int j = i + d;
         float acc = 0.f, acc1 = 0.f;
-        constexpr int MC = 24;
+        constexpr int MB = 8;
+        // both sums read the slot in batches of MB terms, four batches in flight
+        // (a batch's global loads are issued three batches before it is summed)
         if (isq) {
             // qmb: t = 0 .. N-j-5: Y(i, j+5+t) = YR[rowb(i) + d + 1 + t] (LDS),
             // qm1(j+1, j+5+t) on diagonal t+4 at position j (slot, coalesced)
@@ -532,17 +530,41 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
             const int Tq = N - (1 + ls * WAVE + d) - 4;
             const int ta = (Tq * pi) / np, tb = (Tq * (pi + 1)) / np;
             const float *py = L.yr + rowb(i, N) + d + 1;
-            for (int t = ta; t < tb; t += MC) {
-                float q[MC], yv[MC];
+            auto ld = [&](float (&q)[MB], int t) __attribute__((always_inline)) {
 #pragma unroll
-                for (int k = 0; k < MC; k++) q[k] = q1g[off(min(t + k, N - 5) + 4, N) + j];
+                for (int k = 0; k < MB; k++) q[k] = q1g[off(min(t + k, N - 5) + 4, N) + j];
+            };
+            auto use = [&](const float (&q)[MB], int t) __attribute__((always_inline)) {
+                float yv[MB];
 #pragma unroll
-                for (int k = 0; k < MC; k++) yv[k] = py[min(t + k, tb)];
+                for (int k = 0; k < MB; k++) yv[k] = py[t + k];
 #pragma unroll
-                for (int k = 0; k < MC; k += 2) {
+                for (int k = 0; k < MB; k += 2) {
                     acc = fmaf((t + k <= lim && t + k < tb) ? yv[k] : 0.f, q[k], acc);
                     acc1 = fmaf((t + k + 1 <= lim && t + k + 1 < tb) ? yv[k + 1] : 0.f, q[k + 1], acc1);
                 }
+            };
+            float qa[MB], qb[MB], qc[MB], qd[MB];
+            int t = ta;
+            if (t < tb) ld(qa, t);
+            if (t + MB < tb) ld(qb, t + MB);
+            if (t + 2 * MB < tb) ld(qc, t + 2 * MB);
+            while (t < tb) {
+                if (t + 3 * MB < tb) ld(qd, t + 3 * MB);
+                use(qa, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qa, t + 3 * MB);
+                use(qb, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qb, t + 3 * MB);
+                use(qc, t);
+                t += MB;
+                if (t >= tb) break;
+                if (t + 3 * MB < tb) ld(qc, t + 3 * MB);
+                use(qd, t);
+                t += MB;
             }
         } else {
             // r2: u = 5 .. i-1 (ip = i - u): Y(i-u, j) = YR[rowb(i-u) + d + u - 4]
@@ -550,20 +572,22 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
             const int lim = i - 1;
             const int Tr = ilast - 5;
             const int ua = 5 + (Tr * pi) / np, ub = 5 + (Tr * (pi + 1)) / np;
-            for (int u = ua; u < ub; u += MC) {
-                float q[MC], yv[MC];
+            auto ld = [&](float (&q)[MB], int u) __attribute__((always_inline)) {
 #pragma unroll
-                for (int k = 0; k < MC; k++) {
+                for (int k = 0; k < MB; k++) {
                     const int uu = u + k;
                     const bool ok = uu <= lim && uu < ub;
                     q[k] = qmg[off(min(uu, N - 1) - 1, N) + (ok ? i - uu - 1 : 0)];
                 }
+            };
+            auto use = [&](const float (&q)[MB], int u) __attribute__((always_inline)) {
                 // Y(i-u-k, j): the row base moves by (i - u - k - N + 3) per term
                 const int ip0 = max(i - u, 1);
                 const int a0 = rowb(ip0, N) + d + u - 4;
                 const int D0 = i - u - N + 3;
+                float yv[MB];
 #pragma unroll
-                for (int k = 0; k < MC; k++) {
+                for (int k = 0; k < MB; k++) {
                     const int uu = u + k;
                     const bool ok = uu <= lim && uu < ub;
                     const int a = a0 + k * D0 - (k * (k - 1)) / 2;
@@ -571,10 +595,32 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
                     yv[k] = ok ? yv[k] : 0.f;
                 }
 #pragma unroll
-                for (int k = 0; k < MC; k += 2) {
+                for (int k = 0; k < MB; k += 2) {
                     acc = fmaf(yv[k], q[k], acc);
                     acc1 = fmaf(yv[k + 1], q[k + 1], acc1);
                 }
+            };
+            float qa[MB], qb[MB], qc[MB], qd[MB];
+            int u = ua;
+            if (u < ub) ld(qa, u);
+            if (u + MB < ub) ld(qb, u + MB);
+            if (u + 2 * MB < ub) ld(qc, u + 2 * MB);
+            while (u < ub) {
+                if (u + 3 * MB < ub) ld(qd, u + 3 * MB);
+                use(qa, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qa, u + 3 * MB);
+                use(qb, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qb, u + 3 * MB);
+                use(qc, u);
+                u += MB;
+                if (u >= ub) break;
+                if (u + 3 * MB < ub) ld(qc, u + 3 * MB);
+                use(qd, u);
+                u += MB;
             }
         }
         return acc + acc1;

@@ -451,9 +451,9 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 float *gout) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int wb = blockIdx.x / ka.n_groups2, grp = blockIdx.x % ka.n_groups2;
-    const int w = (ka.order && wb < W) ? ka.order[wb] : wb;   // heaviest refolds first
-    if (w >= W) return;
-    if (mask && mask[w] != 1) return;
+    if (wb >= W) return;
+    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
+    if (w < 0) return;
     const int vs0 = ka.groups2[2 * grp], vs1 = ka.groups2[2 * grp + 1];
     const DevVariant V = ka.variants[vs0];
     const bool hol0 = ka.variants[vs0].motif != 0, hol1 = ka.variants[vs1].motif != 0;
@@ -889,19 +889,22 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         // the split points t = 5..T only; the unpaired part is the
                         // column recursion U(i, jb) = qm1(i, jb) + [up_i >= 1] (expMLbase
                         // sigma) U(i+1, jb), U of span sq - 1 kept by the Q wave
-                        const int nb = T - 4;
-                        const int tch = nb > 0 ? (nb + K - 1) / K : 0;   // split points per lane
-                        const int t0 = 5 + k * tch, t1 = min(T, t0 + tch - 1);
+                        // split points interleaved over the K lanes (lane k: t = 5 + k + K m),
+                        // so an item's lanes read consecutive words of its qm1 column and qm
+                        // row (no bank conflicts inside an item)
+                        const int nit = T >= 5 ? (T - 4 + 2 * K - 1) / (2 * K) : 0;
                         const f2 *pq = L.q1 + colb(jb) + i - 1;   // qm1(i+t, jb) at +t
                         const f2 *pr = L.qm + rowb(i, N) - 5;      // qm(i, i+t-1) at +t (t >= 5)
                         const bool up1 = sq >= 5 && (!constrained || L.up[i] >= 1);
                         const f2 u1 = up1 ? L.uc[((sq - 1) & 1) * NP + jb] : f2{0.f, 0.f};
                         const f2 q0 = pq[0];
                         f2 A = {0.f, 0.f}, A1 = {0.f, 0.f};
-                        for (int t = t0; t <= t1; t += 2) {   // pairs: even offsets in A, odd in A1
-                            const f2 qa = pq[t], qn = pq[t + 1], ra = pr[t], rn = pr[t + 1];
-                            A = fma2(ra, qa, A);
-                            A1 = fma2(rn, t + 1 <= t1 ? qn : f2{0.f, 0.f}, A1);
+                        const f2 z = {0.f, 0.f};
+                        for (int m = 0; m < nit; m++) {   // t in A, t + K in A1 (past T: 0, whatever was read)
+                            const int t = 5 + k + 2 * K * m, t2 = t + K;
+                            const f2 qa = pq[t], qn = pq[t2], ra = pr[t], rn = pr[t2];
+                            A = fma2(t <= T ? ra : z, t <= T ? qa : z, A);
+                            A1 = fma2(t2 <= T ? rn : z, t2 <= T ? qn : z, A1);
                         }
                         A += A1;
                         if (K >= 2) A = dpp_add2<0xb1>(A);     // quad_perm [1,0,3,2]

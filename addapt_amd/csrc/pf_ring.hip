@@ -382,10 +382,10 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ng = 2 * ka.n_groups2;
     const int wb = blockIdx.x / ng, rem = blockIdx.x % ng;
-    const int w = (ka.order && wb < W) ? ka.order[wb] : wb;   // heaviest refolds first (kernels.hip order_kernel)
     const int grp = rem >> 1, half = rem & 1;
-    if (w >= W) return;
-    if (mask && mask[w] != 1) return;
+    if (wb >= W) return;
+    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
+    if (w < 0) return;
     const int v0 = ka.groups2[2 * grp], vh = ka.groups2[2 * grp + half];
     if (half == 1 && vh == v0) return;   // a lone variant: one fold
     const DevVariant V = ka.variants[vh];
