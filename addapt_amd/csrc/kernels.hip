@@ -1739,6 +1739,15 @@ __device__ void mt_twist_wave(uint32_t *mt, int lane) {
     }
 }
 
+// Orders a wave's LDS accesses around it (the LDS executes one wave's
+// instructions in order; this keeps the compiler from moving them across):
+// the MC step's waves each own their LDS and never wait for one another.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // A walker's MT19937 stream (MT_WORDS words in HBM: state + index) as a step
 // reads it: only the words [lo, hi) it will draw are staged in LDS (a step
 // draws a few), the whole state only when it twists (then written back).
@@ -1753,7 +1762,7 @@ __device__ uint32_t mt_next(MtView &g, int lane) {
     if (g.idx >= 624) {
         if (g.lo != 0 || g.hi != 624) {
             for (int k = lane; k < 624; k += WAVE) g.mt[k] = g.g[k];
-            __syncthreads();
+            wave_sync();
             g.lo = 0;
             g.hi = 624;
         }
@@ -1899,6 +1908,17 @@ __device__ void nth_element_libstdcxx(double *a, int k, int n) {
 // weight class (fold_class, for order_kernel).  The MC state stays out of the
 // fold kernels' register allocation.
 
+// What a tail reads that nothing in it writes, loaded in one batch at its top
+// (the decision's and the proposal's chains then wait on LDS and on the
+// move tables only)
+struct TailIn {
+    int err = 0, changed = 0, ovf = 0, tabv = 0;
+    double ps = 0.0, cs = 0.0, temp = 1.0, u = 0.0;
+    int ia = 624, ic = 624;   // MT stream indices
+    int ntrain = 0;
+    double auto_T = 0.0, last_diff = 0.0;
+};
+
 struct Accepted {
     bool ran = false;       // a decision was taken (no move error)
     bool changed = false;   // the proposal was scored: last_diff = diff
@@ -1913,41 +1933,33 @@ struct Accepted {
 // (imported configuration, MFE fold outside the 16-bit range) refolds
 // incrementally again -- unless this very fold left the 16-bit range (ovf,
 // MFE: its slot is not exact).  Every lane takes the (uniform) decision, lane 0
-// writes the walker's state, and an accepted proposal's sequence is copied by
-// the whole wave (coalesced).
+// writes the walker's state; the accepted sequence is copied by the tail.
 // kc (comb set): the step's fold launches left the proposal's score as
 // per-variant energies (KArgs::defer_comb): combined here (combine_wave) and
 // stored, but for an MFE fold the FP32 fallback redid (ovf; it stored the score).
 __device__ Accepted accept_walker(const StepArgs &st, const KArgs &kc, bool comb, double *tv, int w, int lane, int s,
-                                  int nt_tot) {
+                                  int nt_tot, const TailIn &in) {
     Accepted a;
-    if (st.err[w]) return a;
+    if (in.err) return a;
     a.ran = true;
-    const bool changed = st.changed[w] == 1;
+    const bool changed = in.changed == 1;
     int outcome = 2;  // ACCEPT_UNCHANGED
-    double prop;
-    if (changed && comb && !(st.ovf && st.ovf[w])) {
+    double prop = in.ps;
+    if (changed && comb && !in.ovf) {
         prop = combine_wave(kc, w, lane, tv ? tv + size_t(w) * nt_tot : nullptr);
         if (lane == 0) st.prop_score[w] = prop;
-    } else {
-        prop = st.prop_score[w];
     }
     double diff = 0.0;
     if (changed) {
-        diff = prop - st.cur_score[w];
-        const double crit = exp(diff / st.temp[w]);
-        outcome = (crit < st.u[w]) ? 0 : (diff > 0) ? 3 : 1;
+        diff = prop - in.cs;
+        const double crit = exp(diff / in.temp);
+        outcome = (crit < in.u) ? 0 : (diff > 0) ? 3 : 1;
     }
     a.changed = changed;
     a.diff = diff;
     const bool acc = outcome == 1 || outcome == 3;
     a.took = acc;
-    if (acc) {
-        const uint8_t *p = st.prop_seq + size_t(w) * st.Nraw;
-        uint8_t *c = st.cur_seq + size_t(w) * st.Nraw;
-        for (int k = lane; k < st.Nraw; k += WAVE) c[k] = p[k];
-        if (st.cur_slot) a.tab_valid = (st.ovf && st.ovf[w]) ? 0 : 1;
-    }
+    if (acc && st.cur_slot) a.tab_valid = in.ovf ? 0 : 1;
     if (lane == 0) {
         if (changed) st.last_diff[w] = diff;
         if (acc) {
@@ -1962,8 +1974,8 @@ __device__ Accepted accept_walker(const StepArgs &st, const KArgs &kc, bool comb
             const size_t r = size_t(s) * st.W + w;
             st.tr_outcome[r] = outcome;
             st.tr_prop[r] = changed ? prop : __builtin_nan("");
-            st.tr_cur[r] = acc ? prop : st.cur_score[w];
-            st.tr_u[r] = changed ? st.u[w] : __builtin_nan("");
+            st.tr_cur[r] = acc ? prop : in.cs;
+            st.tr_u[r] = changed ? in.u : __builtin_nan("");
             if (!changed && st.tr_terms)
                 for (int k = 0; k < nt_tot; k++) st.tr_terms[r * nt_tot + k] = __builtin_nan("");
         }
@@ -1976,19 +1988,18 @@ struct Proposed {
     int plo = -1, phi = -1;
 };
 
-// The proposal of step `step` (trace row s).  acc: the decision this wave just
-// took -- an accepted proposal is read where it is (prop_seq) rather than from
-// the copy the wave just wrote, and the score difference is the auto
-// thermostat's training value.  mt: 2 * MT_WORDS words of LDS.
+// The proposal of step `step` (trace row s).  seq: the walker's current
+// sequence, staged in LDS by the tail (the proposal of the step before when
+// acc took it); acc's score difference is the auto thermostat's training
+// value.  a, c: the streams, their next words staged by the tail (MtView).
 __device__ Proposed propose_walker(const StepArgs &st, long long step, int s, int w, int lane, const Accepted &acc,
-                                   uint32_t *mt) {
+                                   const TailIn &in, const uint8_t *seq, MtView &a, MtView &c) {
     Proposed out;
-    if (st.err[w]) {
+    if (in.err) {
         if (lane == 0) st.changed[w] = 0;
         return out;
     }
     uint8_t *prop = st.prop_seq + size_t(w) * st.Nraw;
-    const uint8_t *cur = acc.took ? prop : st.cur_seq + size_t(w) * st.Nraw;
     uint32_t *gA = st.mtA + size_t(w) * MT_WORDS;
     uint32_t *gC = st.mtC + size_t(w) * MT_WORDS;
     // ---- thermostat (sampling.cc:59; 309-401)
@@ -2000,11 +2011,11 @@ __device__ Proposed propose_walker(const StepArgs &st, long long step, int s, in
         T = ((st.t_lo - st.t_hi) / Nc) * double(int(step % Nc)) + st.t_hi;
     } else {
         double *tr = st.train + size_t(w) * st.period;
-        const int n = st.ntrain[w] + 1;
-        T = st.auto_T[w];
+        const int n = in.ntrain + 1;
+        T = in.auto_T;
         double Tn = T;
         if (lane == 0) {
-            tr[n - 1] = acc.changed ? acc.diff : st.last_diff[w];
+            tr[n - 1] = acc.changed ? acc.diff : in.last_diff;
             if (n >= st.period) {
                 // median = std::nth_element at n/2, clamp = std::max(t, 0.0)
                 // (sampling.cc:389-396): the libstdc++ selection, so -0.0 / NaN
@@ -2021,27 +2032,18 @@ __device__ Proposed propose_walker(const StepArgs &st, long long step, int s, in
         }
         T = __shfl(Tn, 0, WAVE);
     }
-    // ---- move: stream A (and C if the step will be scored); the next 8 words of
-    // each stream staged (a step draws 2 + 2 but for a rejection)
-    uint32_t *mA = mt, *mC = mt + MT_WORDS;
-    const int ia = int(gA[624]), ic = int(gC[624]);
-    if (lane < 8) {
-        if (ia + lane < 624) mA[ia + lane] = gA[ia + lane];
-    } else if (lane < 16) {
-        if (ic + lane - 8 < 624) mC[ic + lane - 8] = gC[ic + lane - 8];
-    }
-    __syncthreads();
-    MtView a{mA, gA, ia, ia, min(ia + 8, 624), false}, c{mC, gC, ic, ic, min(ic + 8, 624), false};
+    // ---- move: stream A (and C if the step will be scored)
     const int pick = int(mt_uniform(a, uint32_t(st.M), lane));
     const int bcode = int(mt_uniform(a, 4u, lane)) + 1;  // "ACGU"[r]
     const int e = st.clo_err[pick];
+    const int k0 = st.clo_off[pick], k1 = st.clo_off[pick + 1];
     bool changed = false;
     int plo = 1 << 30, phi = -1;   // hull of the positions whose base changes (incremental folds)
     if (e == 0) {
-        for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE) {
+        for (int k = k0 + lane; k < k1; k += WAVE) {
             const int pos = st.clo_pos[k];
             const int nb = st.clo_par[k] ? 5 - bcode : bcode;
-            if (cur[pos] != nb) {
+            if (seq[pos] != nb) {
                 changed = true;
                 plo = min(plo, pos);
                 phi = max(phi, pos);
@@ -2057,15 +2059,17 @@ __device__ Proposed propose_walker(const StepArgs &st, long long step, int s, in
     double u = 0.0;
     if (e == 0 && changed) u = mt_canonical(c, lane);
     if (a.twisted)
-        for (int k = lane; k < 624; k += WAVE) gA[k] = mA[k];
+        for (int k = lane; k < 624; k += WAVE) gA[k] = a.mt[k];
     if (c.twisted)
-        for (int k = lane; k < 624; k += WAVE) gC[k] = mC[k];
+        for (int k = lane; k < 624; k += WAVE) gC[k] = c.mt[k];
     if (changed) {
-        if (!acc.took)
-            for (int k = lane; k < st.Nraw; k += WAVE) prop[k] = cur[k];
-        __syncthreads();
-        for (int k = st.clo_off[pick] + lane; k < st.clo_off[pick + 1]; k += WAVE)
-            prop[st.clo_pos[k]] = uint8_t(st.clo_par[k] ? 5 - bcode : bcode);
+        // the proposal: the staged sequence with the move's positions replaced
+        for (int k = lane; k < st.Nraw; k += WAVE) {
+            uint8_t b = seq[k];
+            for (int q = k0; q < k1; q++)
+                if (st.clo_pos[q] == k) b = uint8_t(st.clo_par[q] ? 5 - bcode : bcode);
+            prop[k] = b;
+        }
     }
     if (lane == 0) {
         gA[624] = uint32_t(a.idx);
@@ -2106,24 +2110,86 @@ __device__ __forceinline__ int fold_class(const StepArgs &st, const Proposed &p,
 }
 
 // One wave per walker: the decision of step s_acc (< 0: none, the first
-// proposal of a launch; comb, tv: accept_walker) and the proposal of global step `step` (< 0: none, the
-// last step of a launch; trace row s_prop).  Across a launch_steps call the
-// two halves of a step meet only through HBM written by the launches between.
-__global__ void __launch_bounds__(64) step_tail_kernel(StepArgs st, KArgs kc, int comb, double *tv, int s_acc,
-                                                        long long step, int s_prop, int nt_tot) {
-    __shared__ uint32_t mt[2 * MT_WORDS];
-    const int w = blockIdx.x;
-    const int lane = threadIdx.x;
+// proposal of a launch; comb, tv: accept_walker) and the proposal of global
+// step `step` (< 0: none, the last step of a launch; trace row s_prop).
+// Across a launch_steps call the two halves of a step meet only through HBM
+// written by the launches between.  The walker's scalars, its current and
+// proposed sequences and its MT streams' next words are loaded in one batch
+// first; the sequence the proposal starts from is staged in LDS.
+constexpr int TAIL_NMAX = 256;   // sequences staged whole (launch_steps: Nraw <= TAIL_NMAX)
+constexpr int TAIL_WPB = 4;      // walkers (waves) per workgroup
+__global__ void __launch_bounds__(TAIL_WPB * 64) step_tail_kernel(StepArgs st, KArgs kc, int comb, double *tv,
+                                                                  int s_acc, long long step, int s_prop, int nt_tot) {
+    __shared__ uint32_t mts[TAIL_WPB][2 * MT_WORDS];
+    __shared__ uint8_t seqs[TAIL_WPB][TAIL_NMAX];
+    const int wv = int(threadIdx.x) >> 6;
+    const int w = int(blockIdx.x) * TAIL_WPB + wv;
+    const int lane = int(threadIdx.x) & (WAVE - 1);
+    if (w >= st.W) return;   // no workgroup barrier below: each wave owns its walker and LDS
+    uint32_t *mt = mts[wv];
+    uint8_t *seq = seqs[wv];
+    const int Nr = st.Nraw;
+    uint32_t *gA = st.mtA + size_t(w) * MT_WORDS;
+    uint32_t *gC = st.mtC + size_t(w) * MT_WORDS;
+    const uint8_t *curg = st.cur_seq + size_t(w) * Nr, *propg = st.prop_seq + size_t(w) * Nr;
+    TailIn in;
+    in.err = st.err[w];
+    in.changed = st.changed[w];
+    in.ps = st.prop_score[w];
+    in.cs = st.cur_score[w];
+    in.temp = st.temp[w];
+    in.u = st.u[w];
+    in.ovf = st.ovf ? st.ovf[w] : 0;
+    in.tabv = st.tab_valid ? st.tab_valid[w] : 0;
+    in.ia = int(gA[624]);
+    in.ic = int(gC[624]);
+    if (st.thermo_kind == 2) {
+        in.ntrain = st.ntrain[w];
+        in.auto_T = st.auto_T[w];
+        in.last_diff = st.last_diff[w];
+    }
+    constexpr int SP = TAIL_NMAX / WAVE;   // bytes a lane holds, packed (position q * 64 + lane in byte q)
+    uint32_t cb = 0, pb = 0;
+#pragma unroll
+    for (int q = 0; q < SP; q++) {
+        const int k = q * WAVE + lane;
+        cb |= uint32_t(k < Nr ? curg[k] : 0) << (8 * q);
+        pb |= uint32_t((k < Nr && s_acc >= 0) ? propg[k] : 0) << (8 * q);
+    }
+    // the streams' next 8 words (a step draws 2 + 2 but for a rejection: past
+    // the window MtView reads HBM, at a twist it stages the whole state)
+    if (step >= 0) {
+        if (lane < 8) {
+            if (in.ia + lane < 624) mt[in.ia + lane] = gA[in.ia + lane];
+        } else if (lane < 16) {
+            if (in.ic + lane - 8 < 624) mt[MT_WORDS + in.ic + lane - 8] = gC[in.ic + lane - 8];
+        }
+    }
     Accepted acc;
-    if (s_acc >= 0) acc = accept_walker(st, kc, comb != 0, tv, w, lane, s_acc, nt_tot);
+    if (s_acc >= 0) {
+        acc = accept_walker(st, kc, comb != 0, tv, w, lane, s_acc, nt_tot, in);
+        if (acc.took) {   // the proposal becomes the current sequence
+            uint8_t *c = st.cur_seq + size_t(w) * Nr;
+#pragma unroll
+            for (int q = 0; q < SP; q++) {
+                const int k = q * WAVE + lane;
+                if (k < Nr) c[k] = uint8_t(pb >> (8 * q));
+            }
+        }
+    }
     if (step < 0) return;
-    const Proposed p = propose_walker(st, step, s_prop, w, lane, acc, mt);
+#pragma unroll
+    for (int q = 0; q < SP; q++) {
+        const int k = q * WAVE + lane;
+        if (k < Nr) seq[k] = uint8_t((acc.took ? pb : cb) >> (8 * q));
+    }
+    wave_sync();
+    MtView a{mt, gA, in.ia, in.ia, min(in.ia + 8, 624), false};
+    MtView c{mt + MT_WORDS, gC, in.ic, in.ic, min(in.ic + 8, 624), false};
+    const Proposed p = propose_walker(st, step, s_prop, w, lane, acc, in, seq, a, c);
     if (lane == 0) {
         if (st.ovf) st.ovf[w] = 0;   // set again by this proposal's fold if it leaves the 16-bit range
-        if (st.cls) {
-            const int tabv = !st.tab_valid ? 0 : acc.tab_valid >= 0 ? acc.tab_valid : st.tab_valid[w];
-            st.cls[w] = uint8_t(fold_class(st, p, tabv));
-        }
+        if (st.cls) st.cls[w] = uint8_t(fold_class(st, p, acc.tab_valid >= 0 ? acc.tab_valid : in.tabv));
     }
 }
 
@@ -2532,13 +2598,14 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
 // step_tail_kernel (its decisions and the next step's proposals).
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st0, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
+    if (st0.Nraw > TAIL_NMAX) return hipErrorInvalidValue;
     StepArgs st = st0;
     st.cur_slot = ka.tab ? ka.cur_slot : nullptr;
     st.tab_valid = ka.tab ? ka.tab_valid : nullptr;
     st.ovf = ka.mode == 1 ? ka.ovf : nullptr;
     st.cls = ka.order ? const_cast<uint8_t *>(ka.ocls) : nullptr;   // ordering off: ADX_NO_ORDER / no stored tables
-    hipLaunchKernelGGL(step_tail_kernel, dim3(st.W), dim3(64), 0, stream, st, ka, 0, (double *)nullptr, -1, st.step0,
-                       0, nt_tot);
+    const dim3 tg((st.W + TAIL_WPB - 1) / TAIL_WPB), tb(TAIL_WPB * 64);
+    hipLaunchKernelGGL(step_tail_kernel, tg, tb, 0, stream, st, ka, 0, (double *)nullptr, -1, st.step0, 0, nt_tot);
     KArgs kas = ka;
     kas.defer_comb = 1;   // the tails combine the scores the windows leave as energies
     const int comb = window_defers(kas) ? 1 : 0;
@@ -2547,8 +2614,8 @@ hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st0, hipStream_t 
         hipError_t e = launch_window(kas, st, st.changed, tv, stream, evs ? evs + 4 * s : nullptr);
         if (e != hipSuccess) return e;
         const bool more = s + 1 < st.nsteps;
-        hipLaunchKernelGGL(step_tail_kernel, dim3(st.W), dim3(64), 0, stream, st, kas, comb, tv, s,
-                           more ? st.step0 + s + 1 : -1LL, s + 1, nt_tot);
+        hipLaunchKernelGGL(step_tail_kernel, tg, tb, 0, stream, st, kas, comb, tv, s, more ? st.step0 + s + 1 : -1LL,
+                           s + 1, nt_tot);
     }
     return hipGetLastError();
 }

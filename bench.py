@@ -215,7 +215,7 @@ def executed_inside_work(eng, cur_seqs, tmpl, active, fold, sample=32):
     One traced step after the timed region (its state is not reused): for up
     to `sample` scored proposals, the proposal's sequence is the walker's
     current one with the move applied, the refolded band is the hull of the
-    positions whose base changed (kernels.hip propose_kernel -> chg), and the
+    positions whose base changed (kernels.hip step_tail_kernel -> chg), and the
     band's terms are counted per cell (roofline.cell_terms / band_terms) for
     the 4 folds (apo / holo x unconstrained / active).  Returns (mean executed
     work per scored step, mean full-fold work of the same proposals, proposals

@@ -1,7 +1,7 @@
 """Walkers whose configurations were replaced (adx_walkers_import: the
 replica-exchange swap of BASELINE config 5) fold from scratch until a proposal
 of theirs is accepted; from then on they refold incrementally on that
-proposal's tables (accept_kernel revalidates them).  After the import and 30
+proposal's tables (the step tail's accept revalidates them).  After the import and 30
 more steps every stored score must equal a from-scratch fold of the walker's
 configuration by the step's own kernels (adx_walkers_rescore), bit for bit,
 and equal the oracle's score (the bound of tests/parity_bounds.py)."""
