@@ -849,13 +849,15 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         switch (wid) {
             // blocks of about equal LDS cost per lane-set (a size >= 6: 3 reads for
             // its special shapes + one per 4 generic ones; the small sizes ~3 per shape)
-            case 0: pb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 1: pb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            // (round 5: 9, 13, 14 moved off the waves the stamps showed busiest,
+            // profiles/r05w_pf_cells_stamps.txt: +0.7 %, profiles/r05_ab r05x)
+            case 0: pb_sweep<5, 22, 12, 11, 9>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<4, 21, 19, 10, 14>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 2: pb_sweep<3, 20, 18, 8, 6>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 3: pb_sweep<28, 26, 1, 9, 7>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 4: pb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            case 5: pb_sweep<30, 2, 17, 14, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-            default: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<28, 26, 1, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 16, 0, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            default: pb_sweep<24, 25, 23, 15, 13>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
     } else {
         // the M / F / Q / R chains set the step time; issue arbitration favours the
