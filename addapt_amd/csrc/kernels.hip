@@ -2331,14 +2331,14 @@ const char *inside_kernel_name(const KArgs &ka) {
             KArgs k16 = ka;
             k16.T = ka.T16;
             k16.X = ka.X16;
-            return mfe_pair_active(k16) ? "mfe_pair_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)"
-                                        : "mfe_cells_kernel + combine_kernel + score_kernel<MinPlus> (FP32 fallback launch)";
+            return mfe_pair_active(k16) ? "mfe_pair_kernel + score_kernel<MinPlus> (FP32 fallback launch); scores combined in step_tail_kernel"
+                                        : "mfe_cells_kernel + score_kernel<MinPlus> (FP32 fallback launch); scores combined in step_tail_kernel";
         }
         case InsideK::MfeRows16: return "score_kernel<" ADX_STR(ADX_NT16) ", 1, MinPlus16> + score_kernel<MinPlus> (FP32 fallback launch)";
         case InsideK::MinPlusP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, MinPlus>";
         case InsideK::MinPlus512: return "score_kernel<512, 1, MinPlus>";
-        case InsideK::PfCells: return "pf_cells_kernel + combine_kernel";
-        case InsideK::PfRing: return "pf_ring_kernel + combine_kernel";
+        case InsideK::PfCells: return "pf_cells_kernel (scores combined in step_tail_kernel)";
+        case InsideK::PfRing: return "pf_ring_kernel (scores combined in step_tail_kernel)";
         case InsideK::SumProdP2: return "score_kernel<" ADX_STR(ADX_NT2) ", 2, SumProd>";
         case InsideK::SumProd768: return "score_kernel<768, 1, SumProd>";
         default: return "score_kernel<512, 1, SumProd>";
