@@ -91,7 +91,7 @@ struct OrLay {
 };
 
 // Multiloop-sum work of a diagonal with nls lane-sets: items qmb(ls) and
-// r2(ls), each cut into np parts (split-point ranges), one part per M wave
+// r2(ls), each cut into np parts (split-point ranges), one or two parts per M wave
 // (8-15; their global loads wait on L2, so the sums get as many waves as the
 // interior loops).  Code: 0 = none, else 1 | isq << 1 | ls << 2 | pi << 4 | (np-1) << 6.
 __host__ __device__ constexpr int mcode(bool isq, int ls, int pi, int np) {
@@ -100,13 +100,18 @@ __host__ __device__ constexpr int mcode(bool isq, int ls, int pi, int np) {
 __device__ __forceinline__ int massign(int nls, int w) {
     constexpr int Q = 1, R = 0;
     if (nls >= 3) {
+        // wave 11 takes two parts: qmb of lane-set 2 (the shortest) and r2 of
+        // lane-set 0 (slot 3 = 11 - 8: the M loop runs massign(nls, w - 8) as a
+        // wave's second part); r2 of lane-set 1 split over 12 and 13 (round 5:
+        // one wave carried it whole, 123 terms where the others had <= 71)
         switch (w) {
             case 8: return mcode(Q, 0, 0, 2);
             case 9: return mcode(Q, 0, 1, 2);
             case 10: return mcode(Q, 1, 0, 1);
             case 11: return mcode(Q, 2, 0, 1);
-            case 12: return mcode(R, 0, 0, 1);
-            case 13: return mcode(R, 1, 0, 1);
+            case 3: return mcode(R, 0, 0, 1);
+            case 12: return mcode(R, 1, 0, 2);
+            case 13: return mcode(R, 1, 1, 2);
             case 14: return mcode(R, 2, 0, 2);
             case 15: return mcode(R, 2, 1, 2);
             default: return 0;
@@ -658,6 +663,8 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
             // ---------------- M: the multiloop-sum parts of diagonal d on this wave
             const int c = massign(nls, wid);
             if (c) L.mlp[(par * OX_NW + wid) * WAVE + lane] = mpart(d, (c & 2) != 0, (c >> 2) & 3, (c >> 4) & 3, (c >> 6) + 1);
+            const int c2 = massign(nls, wid - OR_NB);   // a second part, in the slot of B wave wid - 8
+            if (c2) L.mlp[(par * OX_NW + wid - OR_NB) * WAVE + lane] = mpart(d, (c2 & 2) != 0, (c2 >> 2) & 3, (c2 >> 4) & 3, (c2 >> 6) + 1);
         }
         OSTAMP(4);   // M sums
         lds_barrier();
