@@ -2598,6 +2598,7 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
 // step_tail_kernel (its decisions and the next step's proposals).
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st0, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
+    if (st0.nsteps <= 0) return hipSuccess;   // (the first tail would draw a proposal)
     if (st0.Nraw > TAIL_NMAX) return hipErrorInvalidValue;
     StepArgs st = st0;
     st.cur_slot = ka.tab ? ka.cur_slot : nullptr;
