@@ -588,6 +588,7 @@ struct Problem {
         HIP_TRY(dChg.alloc(size_t(W) * 2));
         HIP_TRY(dOrder.alloc(W));
         HIP_TRY(dCls.alloc(W));
+        HIP_TRY(hipMemsetAsync(dCls.p, 64, W, stream));   // "not scored" until a proposal or rescore sets it
         if (adx_status sg = ensure_gstep(W)) return sg;
         HIP_TRY(hipMemsetAsync(dCur.p, 1, W, stream));     // the initial fold writes slot 0
         HIP_TRY(hipMemsetAsync(dValid.p, 0, W, stream));
