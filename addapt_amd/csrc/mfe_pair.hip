@@ -373,7 +373,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     U.nin = reinterpret_cast<const u32 *>(XS->nin);
     U.N = N;
     const uint32_t aqm = lds_addr(L.qm), aqm1 = lds_addr(L.qm1), ae4 = lds_addr(L.e4);
-    constexpr int L_WAVE = 4;           // the lists two steps ahead (diagonals d+4, d+5) and their B records
+    constexpr int L_WAVE = 1;           // (round 5: wave 1 +0.8 % over wave 4, A/B r05zn/r05zo) the lists two steps ahead (diagonals d+4, d+5) and their B records
     constexpr int Q_WAVE = 3;           // q5 of two columns
     constexpr int fw[2] = {F_WAVE, 6};  // finalize lane-sets 0, 1 (rows 1..64, 64..127): lane-set 1
                                         // (spans < 38) rides on block wave 6

@@ -94,9 +94,9 @@ def scost(u, S):
 ROLES4 = "1:8,3:5,4:10" if NBLK == 7 else ""   # NBLK <= 4: the roles have waves of their own
 # pair kernel (mfe_pair.hip; cycles from tools/mfe_pair_stamps.py at ~4k per
 # unit): the split parts of span d on wave 0 and of d+1 on wave 2, q5 of two
-# columns on wave 3, the lists on wave 4, the finalize's second lane-set
+# columns on wave 3, the lists on wave 1 (round 5; wave 4 before), the finalize's second lane-set
 # (spans < 38) on wave 6; its first lane-set has wave 7 to itself
-PAIR_ROLES4 = "0:22,2:22,3:16,4:22,6:5"
+PAIR_ROLES4 = "0:22,1:22,2:22,3:16,6:5"
 
 
 def umin():
