@@ -1484,20 +1484,28 @@ extern "C" adx_status adx_walkers_export_on(adx_ctx *c, void *dev_seqs, void *de
     return ADX_OK;
 }
 
+// The copies and resets of an import, queued on the engine stream (both import
+// entry points: they differ only in how they order against the caller)
+static hipError_t import_queue(adx_ctx *c, const void *dev_seqs, const void *dev_scores) {
+    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
+    hipError_t e = hipSuccess;
+    if (dev_seqs) e = hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream);
+    if (e == hipSuccess && dev_scores)
+        e = hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream);
+    if (e == hipSuccess && dev_seqs && c->pb.dValid.p)   // new configurations: their next fold starts from scratch
+        e = hipMemsetAsync(c->pb.dValid.p, 0, W, c->pb.stream);
+    return e;
+}
+
 extern "C" adx_status adx_walkers_import_after(adx_ctx *c, const void *dev_seqs, const void *dev_scores,
                                                void *producer_stream) {
     if (!c) return fail(ADX_EINVAL, "adx_walkers_import_after: null context");
     if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
-    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
     // NULL is the null stream (torch's default stream), not "no producer": the
     // engine stream is non-blocking and would not otherwise wait for it
     const hipStream_t other = hipStream_t(producer_stream);
     HIP_TRY(stream_after(c->pb.stream, other));
-    if (dev_seqs) HIP_TRY(hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
-    if (dev_scores)
-        HIP_TRY(hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
-    if (dev_seqs && c->pb.dValid.p)   // new configurations: their next fold starts from scratch
-        HIP_TRY(hipMemsetAsync(c->pb.dValid.p, 0, W, c->pb.stream));
+    HIP_TRY(import_queue(c, dev_seqs, dev_scores));
     // the producer's later writes to the buffers wait for the copies
     HIP_TRY(stream_after(other, c->pb.stream));
     return ADX_OK;
@@ -1506,12 +1514,7 @@ extern "C" adx_status adx_walkers_import_after(adx_ctx *c, const void *dev_seqs,
 extern "C" adx_status adx_walkers_import(adx_ctx *c, const void *dev_seqs, const void *dev_scores) {
     if (!c) return fail(ADX_EINVAL, "adx_walkers_import: null context");
     if (c->W <= 0) return fail(ADX_ESTATE, "no walkers");
-    const size_t W = size_t(c->W), N = size_t(c->pb.Nraw);
-    if (dev_seqs) HIP_TRY(hipMemcpyAsync(c->cur_seq.p, dev_seqs, W * N, hipMemcpyDeviceToDevice, c->pb.stream));
-    if (dev_scores)
-        HIP_TRY(hipMemcpyAsync(c->cur_score.p, dev_scores, W * sizeof(double), hipMemcpyDeviceToDevice, c->pb.stream));
-    if (dev_seqs && c->pb.dValid.p)   // new configurations: their next fold starts from scratch
-        HIP_TRY(hipMemsetAsync(c->pb.dValid.p, 0, W, c->pb.stream));
+    HIP_TRY(import_queue(c, dev_seqs, dev_scores));
     HIP_TRY(hipStreamSynchronize(c->pb.stream));
     return ADX_OK;
 }

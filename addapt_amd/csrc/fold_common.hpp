@@ -27,6 +27,17 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Workgroup OR of v through the LDS word *w, which must hold 0 and have been
+// written before a barrier every thread has passed since.  Replaces
+// __syncthreads_or, whose library implementation adds 256 B of static LDS:
+// with none, the dynamic LDS starts at address 0 and every carve address is a
+// literal the compiler rematerialises instead of keeping it in an SGPR.
+__device__ __forceinline__ bool block_or(int *w, bool v) {
+    if (__ballot(v) != 0 && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(w, 1);
+    __syncthreads();
+    return *w != 0;
+}
+
 // The walker a fold workgroup takes at launch position wb (order: a step's
 // launch order, kernels.hip order_kernel; null: blockIdx order), or -1 when
 // mask (1 = fold) leaves it nothing to fold.
@@ -38,6 +49,21 @@ __device__ __forceinline__ int walker_at(const int *order, const int *mask, int 
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 constexpr int MFE16_FLOOR = -12000;
+// Exactness of the packed 16-bit MFE encoding (kernels.hip MinPlus16): a half
+// >= 0x4000 is "impossible".  A true finite value can only reach that band as
+// a sum of at most two stored values plus loop constants (each < 40.96
+// kcal/mol, i.e. < 0x1000), so while every stored finite value is below
+// MFE16_CEIL = 0x1800 (61.44 kcal/mol) no finite value is ever mistaken for an
+// impossible one; and an impossible operand plus one stored value >= FLOOR
+// stays >= 0x7FFF - 12000 > 0x4000, so no impossible value passes for finite.
+// A fold with a stored half outside [FLOOR, CEIL) -- other than the impossible
+// band [0x4000, 0x7FFF] -- is re-folded by the FP32 kernel (round 6: the
+// ceiling; before, a forced fold above 163.84 kcal/mol read as impossible).
+constexpr int MFE16_CEIL = 0x1800;
+__device__ __forceinline__ bool mfe16_inexact(s16x2 q) {
+    auto out = [](int h) { return h < MFE16_FLOOR || (h >= MFE16_CEIL && h < 0x4000); };
+    return out(q.x) || out(q.y);
+}
 
 // Pair type / reversed type / terminal-AU flag without a memory lookup:
 // PAIR[a][b] for codes a, b in 0..4 (ViennaRNA types 1..6) packed 3 bits per

@@ -1138,7 +1138,7 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
         const int C = ((N - 4) * (N - 3)) >> 1;
         auto chk = [&](float x) {
             const s16x2 q = MinPlus16::v(x);
-            low |= (q.x < MFE16_FLOOR) || (q.y < MFE16_FLOOR);
+            low |= mfe16_inexact(q);
         };
         for (int k = tid; k < C; k += NT) {
             chk(L.qbm[0][k]);
@@ -2116,7 +2116,8 @@ __device__ __forceinline__ int fold_class(const StepArgs &st, const Proposed &p,
 // written by the launches between.  The walker's scalars, its current and
 // proposed sequences and its MT streams' next words are loaded in one batch
 // first; the sequence the proposal starts from is staged in LDS.
-constexpr int TAIL_NMAX = 256;   // sequences staged whole (launch_steps: Nraw <= TAIL_NMAX)
+constexpr int TAIL_NMAX = 256;   // sequences staged whole
+static_assert(NMAX < TAIL_NMAX, "adx_api limits sequences to NMAX: the step tail stages them whole");
 constexpr int TAIL_WPB = 4;      // walkers (waves) per workgroup
 __global__ void __launch_bounds__(TAIL_WPB * 64) step_tail_kernel(StepArgs st, KArgs kc, int comb, double *tv,
                                                                   int s_acc, long long step, int s_prop, int nt_tot) {
@@ -2599,7 +2600,6 @@ static hipError_t launch_window(const KArgs &ka, const StepArgs &st, const int *
 hipError_t launch_steps(const KArgs &ka, bool, const StepArgs &st0, hipStream_t stream, hipEvent_t *evs) {
     const int nt_tot = ka.n_terms * ka.n_ctx_eff;
     if (st0.nsteps <= 0) return hipSuccess;   // (the first tail would draw a proposal)
-    if (st0.Nraw > TAIL_NMAX) return hipErrorInvalidValue;
     StepArgs st = st0;
     st.cur_slot = ka.tab ? ka.cur_slot : nullptr;
     st.tab_valid = ka.tab ? ka.tab_valid : nullptr;

@@ -60,6 +60,15 @@ __device__ __forceinline__ uint32_t lds_addr(T *p) {
     return uint32_t(uintptr_t((lds_char *)(p)));   // generic -> LDS address space
 }
 
+// A pointer to LDS byte address a: kernels without static LDS (no __shared__
+// variables, no library code that declares any -- fold_common.hpp block_or)
+// get their dynamic block at address 0, so a carve of literal addresses needs
+// no SGPR per region (the launcher checks the static size is 0)
+template <class T>
+__device__ __forceinline__ T *lds_at(size_t a) {
+    return (T *)((__attribute__((address_space(3))) char *)(uint32_t(a)));
+}
+
 template <class LT>
 __device__ __forceinline__ bool allowed(const LT &L, int i, int j) {   // kernels.hip allowed()
     const int fi = L.flg[i], fj = L.flg[j];
@@ -69,6 +78,20 @@ __device__ __forceinline__ bool allowed(const LT &L, int i, int j) {   // kernel
     if (pi) return pi == j;
     if (pj) return pj == i;
     return L.enc[i] == L.enc[j];
+}
+
+// The per-size energy records (DevScaled::ku16) through the constant address
+// space: uniform loads from it are scalar (s_load, lgkmcnt).  Through a generic
+// pointer they were flat loads, which count on vmcnt too, so the first record
+// use of a block waited for the block's 1x1..2x2 table prefetches from L2.
+#ifndef ADX_KFLAT
+typedef __attribute__((address_space(4))) const uint32_t kc_u32;
+#else   // A/B knob: the records through a generic pointer (flat loads), as before round 6
+typedef const uint32_t kc_u32;
+#endif
+__device__ __forceinline__ const kc_u32 *kconst(const uint4 *p) { return (const kc_u32 *)(uintptr_t)p; }
+__device__ __forceinline__ uint4 kload(const kc_u32 *p, int k) {   // record k (4 words)
+    return make_uint4(p[4 * k], p[4 * k + 1], p[4 * k + 2], p[4 * k + 3]);
 }
 
 // ---------------------------------------------------------------- interior-loop shapes

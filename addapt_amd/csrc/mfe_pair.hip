@@ -84,6 +84,7 @@ struct CP {
     uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
     uint8_t *cl;           // [3][2 np]: rows of the pairable cells of a step's two diagonals, by step % 3
     int *cnt;              // [3]: cells of the step's first diagonal | of both << 16
+    int *flag;             // [2]: block_or words (constrained, 16-bit range left)
     u32 *rec;              // [3][2][64]: the B cells' setup (rank < 64 over both diagonals) by step % 3:
                            //   i | oc << 8 | A << 16 | B << 24 and mismatchI(oc) | mismatch1n(oc) +
                            //   mismatchI(oc) << 16 (MFE table entries are equal in both halves)
@@ -111,22 +112,23 @@ struct PLay {
     static constexpr size_t BY = CC + al16(C);
     static constexpr size_t CLS = BY + al16(8 * NP);
     static constexpr size_t CNT = CLS + al16(6 * NP);
-    static constexpr size_t REC = CNT + 16;
+    static constexpr size_t FLAG = CNT + 16;
+    static constexpr size_t REC = FLAG + 16;
     static constexpr size_t E4 = REC + 3 * 2 * 64 * 4;
     static constexpr size_t BYTES = E4 + size_t(MFE_E4_MAX) * 16;
-    __device__ static CP carve(char *b) {
+    __device__ static CP carve() {   // LDS addresses as literals (no static LDS: the dynamic block starts at 0)
         CP l;
-        l.qbm = reinterpret_cast<u32 *>(b + QBM);
-        l.qm = reinterpret_cast<u32 *>(b + QM);
-        l.qm1 = reinterpret_cast<u32 *>(b + QM1);
-        l.part = reinterpret_cast<int *>(b + PART);
-        l.mla = reinterpret_cast<u32 *>(b + MLA);
-        l.colmin = reinterpret_cast<u32 *>(b + CMN);
-        l.q5 = reinterpret_cast<u32 *>(b + Q5);
-        l.ct = reinterpret_cast<u32 *>(b + CT);
-        l.dt = reinterpret_cast<u32 *>(b + DT);
-        l.cc = reinterpret_cast<uint8_t *>(b + CC);
-        uint8_t *y = reinterpret_cast<uint8_t *>(b + BY);
+        l.qbm = lds_at<u32>(QBM);
+        l.qm = lds_at<u32>(QM);
+        l.qm1 = lds_at<u32>(QM1);
+        l.part = lds_at<int>(PART);
+        l.mla = lds_at<u32>(MLA);
+        l.colmin = lds_at<u32>(CMN);
+        l.q5 = lds_at<u32>(Q5);
+        l.ct = lds_at<u32>(CT);
+        l.dt = lds_at<u32>(DT);
+        l.cc = lds_at<uint8_t>(CC);
+        uint8_t *y = lds_at<uint8_t>(BY);
         l.S = y;
         l.up = y + NP;
         l.dn = y + 2 * NP;
@@ -135,10 +137,11 @@ struct PLay {
         l.flg = y + 5 * NP;
         l.mat = y + 6 * NP;
         l.raw = y + 7 * NP;
-        l.cl = reinterpret_cast<uint8_t *>(b + CLS);
-        l.cnt = reinterpret_cast<int *>(b + CNT);
-        l.rec = reinterpret_cast<u32 *>(b + REC);
-        l.e4 = reinterpret_cast<u32 *>(b + E4);
+        l.cl = lds_at<uint8_t>(CLS);
+        l.cnt = lds_at<int>(CNT);
+        l.flag = lds_at<int>(FLAG);
+        l.rec = lds_at<u32>(REC);
+        l.e4 = lds_at<u32>(E4);
         l.np = NP;
         return l;
     }
@@ -156,7 +159,9 @@ __device__ __forceinline__ int sext_lo(u32 x) { return int(short(x & 0xFFFFu)); 
 __device__ __forceinline__ int sext_hi(u32 x) { return int(x) >> 16; }
 __device__ __forceinline__ u32 pack2(int lo, int hi) { return (u32(lo) & 0xFFFFu) | (u32(hi) << 16); }
 
-template <int NT, int NM>
+// One instance per wave (WID): every wave's sweep holds only its own interior-loop
+// block and roles, so the registers of the other waves' roles are not live in it
+template <int NT, int NM, int WID>
 __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *__restrict__ XS,
                                               const DevTables *__restrict__ TT, const int *vs, const uint8_t *raw,
                                               const CP &L, u32 &z, bool &bad, const IncM &inc) {
@@ -166,7 +171,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const int N = uni(V.N);
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
-    const int wid = uni(tid / WAVE);
+    constexpr int wid = WID;
     const int NP = L.np;
     const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
 #ifdef ADX_STAMP
@@ -251,7 +256,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         const int C = ((N - 4) * (N - 3)) >> 1;
         for (int k = tid; k < C; k += NT) L.qm[k] = INF16;
     }
-    constrained = __syncthreads_or(constrained);
+    constrained = block_or(L.flag, constrained);
     if (tid == 0) {
         L.S[0] = L.S[N];
         L.S[N + 1] = L.S[1];
@@ -378,9 +383,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     constexpr int fw[2] = {F_WAVE, 6};  // finalize lane-sets 0, 1 (rows 1..64, 64..127): lane-set 1
                                         // (spans < 38) rides on block wave 6
     constexpr int mw[2] = {0, 2};       // the split parts of spans d, d+1
-    int fls = -1;
-    for (int k = 0; k < 2; k++)
-        if (fw[k] == wid) fls = k;
+    constexpr int fls = fw[0] == wid ? 0 : (fw[1] == wid ? 1 : -1);
     const int NP2 = 2 * NP;
     // the pairable cells of diagonals db, db+1 (ranks < P0 on db) and the B records of
     // ranks < 64 into list slot sl (a step's B reads them two steps later: its first
@@ -639,7 +642,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             const int sh = slices(P);
             const int cwl = 6 - sh;
             const int Lb = (P + (1 << cwl) - 1) >> cwl;
-            const int blk = wid;
+            constexpr int blk = wid;
             const int r = lane >> cwl;
             U.d = d;
             U.umax = d - 5 < 30 ? d - 5 : 30;   // d+1's loop sizes; d's last one reads the impossible span 3
@@ -885,16 +888,19 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             const bool w1 = j1 >= 5 && j1 <= N && (!incr || j1 >= m_lo - 1);
             if (w0 || w1) {
                 __builtin_amdgcn_s_setprio(PRIO_ROLE);
-                const int s0 = L.S[j0], s1 = L.S[j1];
-                const int sp0 = (j0 < N) ? L.S[j0 + 1] : 5, sp1 = (j1 < N) ? L.S[j1 + 1] : 5;   // no dangle past N
+                // the last step of an odd N has j1 = N + 1 (w1 false): its chain reads
+                // column N instead, so no read leaves the tables (the result is unused)
+                const int j1r = j1 <= N ? j1 : N;
+                const int s0 = L.S[j0], s1 = L.S[j1r];
+                const int sp0 = (j0 < N) ? L.S[j0 + 1] : 5, sp1 = (j1r < N) ? L.S[j1r + 1] : 5;   // no dangle past N
                 u32 acc0 = INF16, acc1 = INF16;
-                for (int k0 = 1; k0 <= j1 - 4; k0 += WAVE) {
+                for (int k0 = 1; k0 <= j1r - 4; k0 += WAVE) {
                     const int kk = k0 + lane;
-                    const bool ok1 = kk <= j1 - 4, ok0 = kk <= j0 - 4;
+                    const bool ok1 = kk <= j1r - 4, ok0 = kk <= j0 - 4;
                     const int k = ok1 ? kk : 1;
                     const int sk = L.S[k], skm = (k > 1) ? L.S[k - 1] : 5;
                     const u32 q5k = L.q5[k - 1];
-                    const int ix1 = off(j1 - k, N) + k - 1;
+                    const int ix1 = off(j1r - k, N) + k - 1;
                     const int ix0 = off(max(j0 - k, 4), N) + k - 1;
                     const u32 ex1 = L.dt[DT_EXT + ptype(sk, s1) * 36 + skm * 6 + sp1];
                     const u32 ex0 = L.dt[DT_EXT + ptype(sk, s0) * 36 + skm * 6 + sp0];
@@ -939,7 +945,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const int C = ((N - 4) * (N - 3)) >> 1;
     auto chk = [&](u32 x) {
         const s16x2 q = sv(x);
-        low |= (q.x < MFE16_FLOOR) || (q.y < MFE16_FLOOR);
+        low |= mfe16_inexact(q);
     };
     for (int k = tid; k < C; k += NT) {
         chk(L.qbm[k]);
@@ -947,7 +953,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         chk(L.qm1[k]);
     }
     for (int k = tid; k <= N; k += NT) chk(L.q5[k]);
-    bad = __syncthreads_or(low);
+    bad = block_or(L.flag + 1, low);
 }
 
 constexpr int MFE_WPE = (2 * NWV + 3) / 4;
@@ -956,8 +962,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFE_WPE
 mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTables *__restrict__ TT, const uint8_t *seqs,
                 int W, float *gout, const int *mask) {
     // one workgroup per (walker, fold group), as mfe_cells_kernel
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const CP L = PLay<NM>::carve(smem);
+    const CP L = PLay<NM>::carve();
     const int ng = ka.n_groups2;
     const int wb = int(blockIdx.x) / ng, g = int(blockIdx.x) % ng;
     if (wb >= W) return;
@@ -976,6 +981,7 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
         for (int k = threadIdx.x; k < 288; k += NT) L.dt[DT_EXT + k] = bits((&T.ext[0][0][0])[k]);
         for (int k = threadIdx.x; k < 8; k += NT) L.dt[DT_TAU + k] = bits(T.termAU[k]);
         for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
+        if (threadIdx.x < 2) L.flag[threadIdx.x] = 0;
         for (int k = threadIdx.x; k < MFE_E4_SLOTS * 4; k += NT) {
             const int a = MFE_E4_A[k >> 2][k & 3];
             L.e4[k] = a < 0 ? INF16 : XS->ku16[MFE_E4_U[k >> 2]][a];
@@ -1000,7 +1006,16 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     }
     u32 z = INF16;
     bool bad = false;
-    mfe_pair_fold<NT, NM>(ka, XS, TT, vs, L.raw, L, z, bad, inc);
+    switch (uni(int(threadIdx.x) / WAVE)) {
+        case 0: mfe_pair_fold<NT, NM, 0>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 1: mfe_pair_fold<NT, NM, 1>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 2: mfe_pair_fold<NT, NM, 2>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 3: mfe_pair_fold<NT, NM, 3>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 4: mfe_pair_fold<NT, NM, 4>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 5: mfe_pair_fold<NT, NM, 5>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        case 6: mfe_pair_fold<NT, NM, 6>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+        default: mfe_pair_fold<NT, NM, 7>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
+    }
     if (threadIdx.x == 0) {
         const s16x2 q = sv(z);
         const int hv[2] = {q.x, q.y};
@@ -1022,8 +1037,12 @@ static hipError_t launch_pair_nm(const KArgs &ka, const uint8_t *seqs, int W, fl
     auto k = mfe_pair_kernel<NWV * WAVE, NM>;
     static bool configured = false;
     if (!configured) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        // the carve addresses LDS from 0 (lds_at): no static LDS may precede the block
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k));
+        if (e != hipSuccess) return e;
+        if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
         configured = true;
     }
@@ -1038,7 +1057,7 @@ bool mfe_pair_covers(const KArgs &ka) { return ka.Nmax <= 100; }
 
 hipError_t launch_mfe_pair(const KArgs &ka, const uint8_t *seqs, int W, float *gout, const int *mask,
                            hipStream_t stream) {
-    static_assert(PLay<100>::BYTES + 256 <= 80 * 1024, "two 100-nt walkers per CU");
+    static_assert(PLay<100>::BYTES <= 80 * 1024, "two 100-nt walkers per CU");
     if (ka.Nmax <= 64) return launch_pair_nm<64>(ka, seqs, W, gout, mask, stream);
     if (ka.Nmax <= 100) return launch_pair_nm<100>(ka, seqs, W, gout, mask, stream);
     return hipErrorInvalidValue;

@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ADX_LIB") or os.path.join(HERE, "_lib", "libaddapt_gpu.so")
 DEFAULT_PARAMS = os.path.join(HERE, "data", "rna_turner2004_addapt.par")
 
+ABI_VERSION = 4   # include/addapt_gpu.h ADX_ABI_VERSION (v4 renumbered the motif modes)
 OK, EINVAL, EHIP, ECONSTRAINT, EPARAM, ENOMEM, EMOVE, ESTATE, ENODEV, EUNSUPPORTED = range(10)
 APO, HOLO = 0, 1
 THERMO_FIXED, THERMO_ANNEAL, THERMO_AUTO = 0, 1, 2
@@ -90,6 +91,12 @@ def lib():
             raise ImportError("addapt_amd native engine not built: %s missing "
                               "(run __graft_entry__.build())" % LIB_PATH)
         L = C.CDLL(LIB_PATH)
+        # a stale build (or an ADX_LIB ablation library) of another ABI would
+        # silently swap enum meanings (v4: motif AUTO = 0, ADD = 1, REPLACE = 2)
+        got = L.adx_abi_version()
+        if got != ABI_VERSION:
+            raise ImportError("%s has ABI version %d, this binding needs %d (rebuild: "
+                              "__graft_entry__.build())" % (LIB_PATH, got, ABI_VERSION))
         L.adx_last_error.restype = C.c_char_p
         L.adx_kT.restype = C.c_double
         L.adx_params_load.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]

@@ -182,11 +182,15 @@ def dry_run(a, rank, world):
     time.sleep(0.001 * a.steps * (1 + rank))
     if world > 1:
         dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    mine = time.perf_counter() - t0
+    d = dist if world > 1 else None
+    elapsed = shard.max_over_ranks(mine, d)
+    per_rank = shard.gather_over_ranks(mine / max(1, a.steps) * 1e3, d)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": a.walkers * a.steps * world / elapsed,
                           "unit": "MC steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": elapsed / a.steps * 1e3, "dry_run": True,
+                          "dist": shard.dist_record(d, per_rank, elapsed / max(1, a.steps) * 1e3),
                           "ranks": shard.walker_ids(rank, world, a.walkers)[:1]}))
     if world > 1:
         dist.destroy_process_group()
@@ -322,6 +326,7 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     inside_name, outside_name = eng.last_kernel_names()  # what the engine launched
     fin_seqs, fin_scores, c1 = eng.download()
     elapsed = shard.max_over_ranks(t1 - t0, dist, device=dev)
+    per_rank_ms = shard.gather_over_ranks((t1 - t0) / max(1, steps) * 1e3, dist, device=dev)
     if dump:
         import numpy as np
 
@@ -452,6 +457,7 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": elapsed / steps * 1e3,
+        "dist": shard.dist_record(dist, per_rank_ms, elapsed / steps * 1e3),
         "dtype": "i16x2" if fold == "mfe" else "fp32",
         "workload": "%s: default objective (apo: not active, holo: active; THEO aptamer "
                     "0.32 uM)%s, 4 %s%s per scored step, synthetic %d-nt sgRNA template "
@@ -575,6 +581,9 @@ def main():
             "outcomes": rec["outcomes"],
         },
         "roofline": rec["roofline"],
+        # the collective backend torch.distributed ran ("nccl" = RCCL on ROCm), the
+        # world size it reported, each rank's ms per step and their max (the value's clock)
+        "dist": rec["dist"],
     }
     if "exchange" in rec:
         out["exchange"] = rec["exchange"]

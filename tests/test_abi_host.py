@@ -34,7 +34,7 @@ def test_library_exports_every_symbol(native):
 
 
 def test_abi_version_and_kT(native, oracle):
-    assert native.lib().adx_abi_version() >= 1
+    assert native.lib().adx_abi_version() == native.ABI_VERSION == 4
     # scoring.cc:69-70: kT = exp_params->kT / 1000 at 37 C
     assert abs(native.kT() - (37.0 + 273.15) * 1.98717 / 1000.0) < 1e-12
     assert abs(native.kT() - oracle.KT_KCAL) < 1e-12

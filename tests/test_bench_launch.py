@@ -27,6 +27,14 @@ def test_bench_spawns_ranks_gloo():
     assert out["n_gpus"] == 2 and out["dry_run"] and out["steps"] == 3
     # max over ranks: rank 1 sleeps twice as long as rank 0 (2 x 3 ms)
     assert out["ms_per_step"] >= 1.9, out
+    # what ran: the backend and world size torch.distributed reported, per-rank
+    # step times and the max the value is computed from (the driver's SCALE
+    # record reads the same fields with backend "nccl" = RCCL)
+    d = out["dist"]
+    assert d["backend"] == "gloo" and d["library"] == "gloo" and d["world_size"] == 2, d
+    assert len(d["per_rank_ms_per_step"]) == 2
+    assert d["per_rank_ms_per_step"][1] > d["per_rank_ms_per_step"][0], d
+    assert d["max_ms_per_step"] == max(d["per_rank_ms_per_step"]) == out["ms_per_step"], d
 
 
 def test_bench_refuses_more_gpus_than_visible():

@@ -36,6 +36,10 @@ def test_bench_two_ranks_sharded():
     assert sum(out["config"]["outcomes"].values()) == 2 * W * STEPS   # summed over ranks
     assert out["value"] > 0 and out["roofline"]["kernel_ms_per_launch"] > 0
     assert "walker-sharded x2" in out["config"]["parallelism"]
+    d = out["dist"]   # what torch.distributed reported (the RCCL run: backend "nccl")
+    assert d["backend"] == "gloo" and d["world_size"] == 2 and len(d["per_rank_ms_per_step"]) == 2
+    assert d["max_ms_per_step"] == max(d["per_rank_ms_per_step"])
+    assert abs(d["max_ms_per_step"] - out["ms_per_step"]) <= 1e-9 * out["ms_per_step"]
 
 
 @pytest.mark.gpu

@@ -73,6 +73,25 @@ def test_fold_mfe_extreme_energies(native, oracle):
         assert _same(g, ref), (seq, g, ref)
 
 
+def test_fold_mfe_high_positive_energies(native, oracle):
+    """Forced structures far above zero: chains of isolated G-C pairs closing
+    triloops, 3.9 kcal/mol each.  Stored 16-bit values at or above 61.44
+    kcal/mol (fold_common.hpp MFE16_CEIL) send the fold to the FP32 kernel, so
+    results stay bit-exact up to and beyond the 163.84 kcal/mol the 16-bit
+    encoding reads as impossible (before round 6 the 250-nt fold returned +inf).
+    Lengths cover the pair kernel (70, 100), the cells kernel (150) and the
+    general kernel (250)."""
+    for k in (14, 20, 30, 50):
+        seq, cst = "GAAAC" * k, "(...)" * k
+        f = native.Fold(seq)
+        f.add_constraint(cst)
+        g = f.mfe()
+        ref = oracle.mfe_energy(seq, cst)
+        assert ref > 50.0 and not math.isinf(ref)
+        assert _same(g, ref), (len(seq), g, ref)
+    assert oracle.mfe_energy("GAAAC" * 50, "(...)" * 50) > 163.84
+
+
 def test_score_batch_mfe_mixed_fallback(native, oracle):
     """A batch mixing ordinary walkers and GC-rich ones: per-walker fallback."""
     tmpl, active = workloads.synthetic(150)

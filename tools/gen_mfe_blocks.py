@@ -217,9 +217,9 @@ def emit_group_asm(u, out):
                 outs.append('[c%d] "=&v"(c%d)' % (u1, u1))
             # the loop size's energy record: uniform, scalar loads (DevScaled::ku16)
             if need_g:
-                decl.append("        const uint4 kr0 = kg[%d];" % (2 * u))
+                decl.append("        const uint4 kr0 = kload(kg, %d);" % (2 * u))
             if u >= 2:
-                decl.append("        const uint4 kr1 = kg[%d];" % (2 * u + 1))
+                decl.append("        const uint4 kr1 = kload(kg, %d);" % (2 * u + 1))
         lines.append("s_waitcnt lgkmcnt(0)")
         out.append("        {")
         out.extend(decl)
@@ -353,9 +353,9 @@ def sliced_parts(u, S, t):
             ins.append('[qt%s] "v"(C.ee)' % t)
     # the loop size's energy record: uniform, scalar loads (DevScaled::ku16)
     if gen:
-        decl.append("const uint4 kr0%s = kg[%d];" % (t, 2 * u))
+        decl.append("const uint4 kr0%s = kload(kg, %d);" % (t, 2 * u))
     if u >= 2:
-        decl.append("const uint4 kr1%s = kg[%d];" % (t, 2 * u + 1))
+        decl.append("const uint4 kr1%s = kload(kg, %d);" % (t, 2 * u + 1))
     # constrained cells: shapes past the allowed unpaired runs (u1 > A or u2 > B) take no part
     post.append("if (U.mk) {")
     post.append("    const int ml = %d - C.B, mh = C.A, rr = int(C.rs >> 2);" % u)
@@ -501,7 +501,7 @@ def emit_file():
             out.append('    int hb = C.hb;')
             out.append('    asm volatile("" : "+v"(hb));')
         out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
-        out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
+        out.append('    const kc_u32 *kg = kconst(U.kg);   // opaque: the record loads stay at their use (s_load, SGPRs)')
         out.append('    asm volatile("" : "+s"(kg));')
         emit_table_decl(blk, out)
         for u in blk:
@@ -537,7 +537,7 @@ def emit_file():
                 out.append('    int hb = C.hb;')
                 out.append('    asm volatile("" : "+v"(hb));')
             out.append('    asm volatile("" : "+s"(dd), "+s"(um));')
-            out.append('    const uint4 *kg = U.kg;   // opaque: the record loads stay at their use (SGPRs)')
+            out.append('    const kc_u32 *kg = kconst(U.kg);   // opaque: the record loads stay at their use (s_load, SGPRs)')
             out.append('    asm volatile("" : "+s"(kg));')
             emit_table_decl(blk, out)
             emit_block_cells_sliced(blk, S, out)
