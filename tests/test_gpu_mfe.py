@@ -74,22 +74,22 @@ def test_fold_mfe_extreme_energies(native, oracle):
 
 
 def test_fold_mfe_high_positive_energies(native, oracle):
-    """Forced structures far above zero: chains of isolated G-C pairs closing
-    triloops, 3.9 kcal/mol each.  Stored 16-bit values at or above 61.44
+    """Forced structures far above zero: chains of isolated U-G pairs closing
+    triloops, 5.82 kcal/mol each.  Stored 16-bit values at or above 61.44
     kcal/mol (fold_common.hpp MFE16_CEIL) send the fold to the FP32 kernel, so
     results stay bit-exact up to and beyond the 163.84 kcal/mol the 16-bit
-    encoding reads as impossible (before round 6 the 250-nt fold returned +inf).
-    Lengths cover the pair kernel (70, 100), the cells kernel (150) and the
-    general kernel (250)."""
-    for k in (14, 20, 30, 50):
-        seq, cst = "GAAAC" * k, "(...)" * k
+    encoding reads as impossible (before round 6 the 150-nt fold, 174.4
+    kcal/mol, returned +inf).  Lengths cover the pair kernel (70, 100) and the
+    cells kernel (150)."""
+    for k in (14, 20, 30):
+        seq, cst = "UUUUG" * k, "(...)" * k
         f = native.Fold(seq)
         f.add_constraint(cst)
         g = f.mfe()
         ref = oracle.mfe_energy(seq, cst)
-        assert ref > 50.0 and not math.isinf(ref)
+        assert ref > 60.0 and not math.isinf(ref)
         assert _same(g, ref), (len(seq), g, ref)
-    assert oracle.mfe_energy("GAAAC" * 50, "(...)" * 50) > 163.84
+    assert oracle.mfe_energy("UUUUG" * 30, "(...)" * 30) > 163.84
 
 
 def test_score_batch_mfe_mixed_fallback(native, oracle):
