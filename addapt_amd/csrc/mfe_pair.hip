@@ -32,6 +32,7 @@
 
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #include "dev_types.hpp"
 #include "fold_common.hpp"
@@ -52,12 +53,19 @@ namespace {
 // of qm (one span per wave), the lists and q5 ride on block waves, whose loop
 // sizes the generator partitions around them (tools/gen_mfe_blocks.py
 // PAIR_ROLES4; two workgroups per CU)
-constexpr int NWV = 8;
-constexpr int F_WAVE = 7;
+#ifndef ADX_PAIR_NBLK
+#define ADX_PAIR_NBLK 7
+#endif
+constexpr int NWV = ADX_PAIR_NBLK + 1;
+constexpr int F_WAVE = NWV - 1;
 constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
 
+#if ADX_PAIR_NBLK == 7
 #include "mfe_pair_blocks.inc"
-static_assert(MFE_NBLK == 7, "seven block waves");
+#else
+#include "mfe_pair_blocks9.inc"   // A/B: nine block waves (ADX_GEN_PAIR_NBLK=9)
+#endif
+static_assert(MFE_NBLK == ADX_PAIR_NBLK, "one block per block wave");
 
 constexpr int PINF = 32767;   // an impossible half, sign-extended (the partial slots)
 
@@ -956,6 +964,14 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     bad = block_or(L.flag + 1, low);
 }
 
+// the fold instance of wave w (one per wave: mfe_pair_fold's WID)
+template <int NT, int NM, int... Ws>
+__device__ __forceinline__ void pair_fold_wave(std::integer_sequence<int, Ws...>, int w, const KArgs &ka,
+                                               const DevScaled *__restrict__ XS, const DevTables *__restrict__ TT,
+                                               const int *vs, const CP &L, u32 &z, bool &bad, const IncM &inc) {
+    ((w == Ws ? (mfe_pair_fold<NT, NM, Ws>(ka, XS, TT, vs, L.raw, L, z, bad, inc), 0) : 0), ...);
+}
+
 constexpr int MFE_WPE = (2 * NWV + 3) / 4;
 template <int NT, int NM>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MFE_WPE, MFE_WPE)))
@@ -1006,16 +1022,8 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     }
     u32 z = INF16;
     bool bad = false;
-    switch (uni(int(threadIdx.x) / WAVE)) {
-        case 0: mfe_pair_fold<NT, NM, 0>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 1: mfe_pair_fold<NT, NM, 1>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 2: mfe_pair_fold<NT, NM, 2>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 3: mfe_pair_fold<NT, NM, 3>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 4: mfe_pair_fold<NT, NM, 4>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 5: mfe_pair_fold<NT, NM, 5>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        case 6: mfe_pair_fold<NT, NM, 6>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-        default: mfe_pair_fold<NT, NM, 7>(ka, XS, TT, vs, L.raw, L, z, bad, inc); break;
-    }
+    pair_fold_wave<NT, NM>(std::make_integer_sequence<int, NWV>{}, uni(int(threadIdx.x) / WAVE), ka, XS, TT, vs, L, z,
+                           bad, inc);
     if (threadIdx.x == 0) {
         const s16x2 q = sv(z);
         const int hv[2] = {q.x, q.y};

@@ -863,8 +863,12 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         // the M / F / Q / R chains set the step time; issue arbitration favours the
         // older (B) waves of the workgroup, so these run at a higher priority
         __builtin_amdgcn_s_setprio(2);
+        // one sweep instance per role (round 6): each holds only its own role's
+        // registers (the shared loop kept every role's values live: 38 SGPR spills)
+        auto sweep = [&](auto role_c) __attribute__((always_inline)) {
+        constexpr int ROLE = decltype(role_c)::value;   // 0 M, 1 F, 2 Q, 3 R
         for (int s = 4; s <= s_end; s++) {
-            if (px_mw(wid) >= 0) {
+            if constexpr (ROLE == 0) {
                 // ---------------- M: qm items of span sq = s - 2, K lanes per item (a
                 // power of two <= 16, one DPP row), split points in contiguous runs per
                 // lane, summed over the K lanes:
@@ -919,7 +923,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         }
                     }
                 }
-            } else if (wid == PX_WF) {
+            } else if constexpr (ROLE == 1) {
                 // ---------------- F: the changed cells of diagonal e = s - 1
                 const int e = s - 1;
                 if (e >= 4 && e <= N - 1) {
@@ -952,7 +956,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         }
                     }
                 }
-            } else if (wid == PX_WQ) {
+            } else if constexpr (ROLE == 2) {
                 // ---------------- Q: q5[j], j = s - 1 (column j is final); the
                 // exterior factors of column j + 1 are gathered one step ahead
                 const int j = s - 1;
@@ -981,7 +985,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                     }
                 }
                 qfac(j + 1);
-            } else if (wid == PX_WR) {
+            } else {
                 // ---------------- R: records of diagonal s + 2 (B loads them next step for
                 // the step after), tables of s + 3, bases of s + 4, rank list of s + 5
                 rec_store(s + 2, pend);
@@ -993,6 +997,11 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             lds_barrier();
             PSTAMP(6);
         }
+        };
+        if (px_mw(wid) >= 0) sweep(std::integral_constant<int, 0>{});
+        else if (wid == PX_WF) sweep(std::integral_constant<int, 1>{});
+        else if (wid == PX_WQ) sweep(std::integral_constant<int, 2>{});
+        else sweep(std::integral_constant<int, 3>{});   // PX_WR
     }
 #ifdef ADX_STAMP
     if (lane == 0)

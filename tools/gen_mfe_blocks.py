@@ -476,9 +476,19 @@ def emit_block_cells_sliced(blk, S, out):
     emit_table_fin(blk, out)
 
 
+# the pair kernel's block waves (ADX_GEN_PAIR_NBLK; its output file name
+# ADX_GEN_PAIR_OUT, for A/B builds of another wave count)
+PAIR_NBLK = int(os.environ.get("ADX_GEN_PAIR_NBLK", str(NBLK)))
+
+
 def main():
-    global PAIR
+    global PAIR, NBLK
+    cells_nblk = NBLK
+    only = os.environ.get("ADX_GEN_ONLY")   # "pair" / "cells": one file
     for PAIR in (False, True):
+        if only and only != ("pair" if PAIR else "cells"):
+            continue
+        NBLK = PAIR_NBLK if PAIR else cells_nblk
         emit_file()
 
 
@@ -579,7 +589,8 @@ def emit_file():
         "{%s}" % ", ".join(str(-1 if a is None else a) for a in row) for _, _, row in sl) or "{-1, -1, -1, -1}"))
     out.append("constexpr int MFE_NBLK = %d;" % NBLK)
     out.append("constexpr int MFE_KSAT = %d;   // generic loops: nin[k] == nin[MFE_KSAT] for k >= MFE_KSAT" % KSAT)
-    path = os.path.join(out_dir(), "mfe_pair_blocks.inc" if PAIR else "mfe_blocks.inc")
+    path = os.path.join(out_dir(), os.environ.get("ADX_GEN_PAIR_OUT", "mfe_pair_blocks.inc") if PAIR
+                        else "mfe_blocks.inc")
     with open(path, "w") as f:
         f.write("\n".join(out) + "\n")
     print("blocks:", blocks, "load:", load, file=sys.stderr)

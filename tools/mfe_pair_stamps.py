@@ -33,7 +33,9 @@ cols = ["setup", "top", "L", "F", "Bcell", "Bblock", "Bfold", "M", "Q", "barrier
         "s.restore", "s.seq", "s.motif", "s.cells"]
 print("cycles per fold group per wave (N=%d, W=%d, %d steps, %.0f groups)" % (N, W, steps, G))
 print("wave " + " ".join("%8s" % n for n in cols))
-for w in range(8):
+for w in range(16):
+    if not any(buf[w * 16 + k] for k in range(16)):
+        continue
     v = [buf[w * 16 + k] // max(1, G) for k in (8, 0, 1, 2, 9, 10, 3, 4, 5, 6)]
     sub = [buf[w * 16 + k] // max(1, G) for k in (11, 12, 13, 14)]
     print("%4d " % w + " ".join("%8d" % x for x in v) + " %8d" % sum(v) + " " + " ".join("%8d" % x for x in sub))
