@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -90,6 +92,7 @@ struct CP {
     u32 *dt;               // DT_* block (packed)
     uint8_t *cc;           // inner-pair code per cell (diagonal-major), pad before it
     uint8_t *S, *up, *dn, *ptn, *enc, *flg, *mat, *raw;
+    u32 *pos;              // [np]: S | flg << 3 | up << 8 | ptn << 16 | enc << 24 (the per-cell pass)
     uint8_t *cl;           // [3][2 np]: rows of the pairable cells of a step's two diagonals, by step % 3
     int *cnt;              // [3]: cells of the step's first diagonal | of both << 16
     int *flag;             // [2]: block_or words (constrained, 16-bit range left)
@@ -123,7 +126,8 @@ struct PLay {
     static constexpr size_t FLAG = CNT + 16;
     static constexpr size_t REC = FLAG + 16;
     static constexpr size_t E4 = REC + 3 * 2 * 64 * 4;
-    static constexpr size_t BYTES = E4 + size_t(MFE_E4_MAX) * 16;
+    static constexpr size_t POS = E4 + size_t(MFE_E4_MAX) * 16;
+    static constexpr size_t BYTES = POS + al16(size_t(NP) * 4);
     __device__ static CP carve() {   // LDS addresses as literals (no static LDS: the dynamic block starts at 0)
         CP l;
         l.qbm = lds_at<u32>(QBM);
@@ -150,6 +154,7 @@ struct PLay {
         l.flag = lds_at<int>(FLAG);
         l.rec = lds_at<u32>(REC);
         l.e4 = lds_at<u32>(E4);
+        l.pos = lds_at<u32>(POS);
         l.np = NP;
         return l;
     }
@@ -193,20 +198,23 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     auto qlo = [&](int s) { return incr ? max(1, m_lo - 2 - s) : 1; };
     auto qhi = [&](int s) { return incr ? min(N - s, m_hi + 2) : N - s; };
 
-    // ---- refold restore first (8-byte vector loads)
+    // ---- refold restore: the loads of all three tables are issued first (8-byte
+    // vector loads into registers) and stored to LDS after the motif scan, so
+    // their HBM latency overlaps the sequence / motif setup (round 6; the loop of
+    // dependent load -> store pairs cost ~20k cycles per fold group)
+    constexpr int CNM = ((NM - 4) * (NM - 3)) >> 1;
+    constexpr int RS = (3 * (CNM >> 1) + NT - 1) / NT;   // loads per thread
+    const int Crs = ((N - 4) * (N - 3)) >> 1, half = Crs >> 1;
+    uint2 rsv[RS];
     if (incr) {
         const size_t Cs = size_t(ka.cells);
-        const int C = ((N - 4) * (N - 3)) >> 1, half = C >> 1;
-#pragma unroll 8
-        for (int k = tid; k < 3 * half; k += NT) {
-            const int a = k / half, c = k - a * half;
-            const uint2 x = *reinterpret_cast<const uint2 *>(inc.src + a * Cs + 2 * c);
-            u32 *d = a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1;
-            *reinterpret_cast<uint2 *>(d + 2 * c) = x;
+#pragma unroll
+        for (int t = 0; t < RS; t++) {
+            const int k = tid + t * NT;
+            const int kk = k < 3 * half ? k : 0;
+            const int a = kk / half, c = kk - a * half;
+            rsv[t] = *reinterpret_cast<const uint2 *>(inc.src + a * Cs + 2 * c);
         }
-        if (C & 1)
-            for (int a = tid; a < 3; a += NT) (a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1)[C - 1] = inc.src[a * Cs + C - 1];
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) L.q5[k] = inc.src[3 * Cs + k];
     }
     // setup scratch in the partial / split / U slots (first written after the per-cell pass)
     uint32_t *spk = reinterpret_cast<uint32_t *>(L.part);
@@ -242,22 +250,23 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
     }
     bool constrained = false;
+    auto seq_at = [&](int k) -> uint8_t {   // base of position k (1..N)
+        const int pp = k - 1;
+        return pp < blen ? bef[pp] : (pp < blen + ka.Nraw ? raw[pp - blen] : aft[pp - blen - ka.Nraw]);
+    };
     for (int k = tid; k < np; k += NT) {
-        uint8_t s = 0;
-        if (k >= 1 && k <= N) {
-            const int pp = k - 1;
-            if (pp < blen) s = bef[pp];
-            else if (pp < blen + ka.Nraw) s = raw[pp - blen];
-            else s = aft[pp - blen - ka.Nraw];
-        }
+        const uint8_t s = (k >= 1 && k <= N) ? seq_at(k) : 0;
         L.S[k] = s;
-        const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k];
-        L.up[k] = cons[k];
+        const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k], up = cons[k], en = cons[3 * np + k];
+        L.up[k] = up;
         L.dn[k] = cons[np + k];
         L.ptn[k] = pt;
-        L.enc[k] = cons[3 * np + k];
+        L.enc[k] = en;
         L.flg[k] = f;
         L.mat[k] = 0;
+        // ViennaRNA's S1 wrap-around in the words (L.S gets it below)
+        const uint8_t sw = k == 0 ? seq_at(N) : (k == N + 1 ? seq_at(1) : s);
+        L.pos[k] = u32(sw) | (u32(f & 7) << 3) | (u32(up) << 8) | (u32(pt) << 16) | (u32(en) << 24);
         if (k >= 1 && k <= N && (f || pt)) constrained = true;
     }
     if (!incr) {
@@ -306,6 +315,21 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             if (lane == 0) L.mat[o] = all ? 1 : 0;
         }
     }
+    if (incr) {   // the restore's stores (loads issued at the start)
+        const size_t Cs = size_t(ka.cells);
+#pragma unroll
+        for (int t = 0; t < RS; t++) {
+            const int k = tid + t * NT;
+            if (k < 3 * half) {
+                const int a = k / half, c = k - a * half;
+                u32 *d = a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1;
+                *reinterpret_cast<uint2 *>(d + 2 * c) = rsv[t];
+            }
+        }
+        if (Crs & 1)
+            for (int a = tid; a < 3; a += NT) (a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1)[Crs - 1] = inc.src[a * Cs + Crs - 1];
+        for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) L.q5[k] = inc.src[3 * Cs + k];
+    }
     __syncthreads();
     const u32 mlclosing = __float_as_uint(XS->mlclosing);
     const u32 mlbase = __float_as_uint(XS->mlbase_sig);
@@ -320,41 +344,77 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const unsigned long long st_s3 = __builtin_amdgcn_s_memtime();   // motif sites
 #endif
     // ---- per-cell setup (mfe_cells.hip): inner-pair code, hairpin (+ motif) or the
-    // non-pairable mark, multiloop stem of the pairable cells
-    for (int dd = 4 + wid; dd <= N - 1; dd += NWV) {
-        const int od = off(dd, N);
-        const int u = dd - 1;
-        const int lo = clo(dd), hi = chi(dd);
-        for (int r = lane; r < N - dd; r += WAVE) {
-            const int i = r + 1, j = i + dd;
-            const int si = L.S[i], sj = L.S[j], sim = L.S[i - 1], sjp = L.S[j + 1];
-            const int type = ptype(si, sj);
-            L.cc[od + r] = static_cast<uint8_t>(rtype(type) * 25 + sjp * 5 + sim);
-            if (i < lo || i > hi) continue;
-            const bool pr = type != 0 && allowed(L, i, j);
-            u32 h = INF16, m1 = INF16;
-            if (pr) {
-                if (L.up[i + 1] >= u) {
-                    bool special = false;
-                    if (u == 3 || u == 4 || u == 6) {
-                        const uint32_t key = hp_key(L.S, i, u + 2);
-                        for (int q0 = 0; q0 < nsp; q0 += 8) {
+    // non-pairable mark, multiloop stem of the pairable cells.  Round 6: every
+    // lane-set of two diagonals at once, each in two LDS round trips (the
+    // position words, then the mismatch / stem factors), where the one-cell-at-
+    // a-time loop took ~5 dependent round trips per lane-set
+    auto cell_pass = [&](int dd0) __attribute__((always_inline)) {
+        constexpr int NI = 4;   // items: (dd0, dd0 + NWV) x lane-sets 0, 1
+        int ii[NI], jj[NI], dv[NI];
+        bool ok[NI];
+        u32 wim[NI], wi[NI], wi1[NI], wjm[NI], wj[NI], wjp[NI];
+        uint32_t mt[NI];
 #pragma unroll
-                            for (int t = 0; t < 8; t++)
-                                if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
-                        }
-                    }
-                    if (!special)
-                        h = padd(__float_as_uint(XS->hp[u]), (u == 3) ? L.dt[DT_TAU + type]
-                                                           : L.dt[DT_MMH + type * 25 + L.S[i + 1] * 5 + L.S[j - 1]]);
-                }
-                if (dd == mL - 1 && mL > 0 && L.mat[i]) h = pmin(h, mextra);
-                m1 = L.dt[DT_MLS + type * 25 + sim * 5 + sjp];
-            }
-            L.qbm[od + r] = pr ? h : MARK16;
-            L.qm1[colb(j) + i - 1] = m1;
+        for (int q = 0; q < NI; q++) {
+            const int d = dd0 + (q >> 1) * NWV;
+            const int r = lane + (q & 1) * WAVE;
+            dv[q] = d;
+            ok[q] = d <= N - 1 && r < N - d;
+            const int i = ok[q] ? r + 1 : 1, j = ok[q] ? i + d : 5;
+            ii[q] = i;
+            jj[q] = j;
+            wim[q] = L.pos[i - 1];
+            wi[q] = L.pos[i];
+            wi1[q] = L.pos[i + 1];
+            wjm[q] = L.pos[j - 1];
+            wj[q] = L.pos[j];
+            wjp[q] = L.pos[j + 1];
+            mt[q] = L.mat[i];
         }
-    }
+        int ty[NI], ix1[NI];
+        bool pr[NI], inb[NI];
+        u32 f1[NI], f2[NI];
+#pragma unroll
+        for (int q = 0; q < NI; q++) {
+            const int i = ii[q], j = jj[q], d = dv[q];
+            const int si = wi[q] & 7, sj = wj[q] & 7;
+            ty[q] = ptype(si, sj);
+            inb[q] = ok[q] && i >= clo(d) && i <= chi(d);
+            const int fi = (wi[q] >> 3) & 7, fj = (wj[q] >> 3) & 7;
+            const int pi = (wi[q] >> 16) & 255, pj = (wj[q] >> 16) & 255;
+            bool al = !((fi | fj) & 1) && !((fi & 2) || (fj & 4));
+            al = al && (pi ? pi == j : (pj ? pj == i : (wi[q] >> 24) == (wj[q] >> 24)));
+            pr[q] = inb[q] && ty[q] != 0 && al;
+            const int sim = wim[q] & 7, sjp = wjp[q] & 7, si1 = wi1[q] & 7, sjm = wjm[q] & 7;
+            ix1[q] = (d - 1 == 3) ? DT_TAU + ty[q] : DT_MMH + ty[q] * 25 + si1 * 5 + sjm;
+            f1[q] = L.dt[ix1[q]];
+            f2[q] = L.dt[DT_MLS + ty[q] * 25 + sim * 5 + sjp];
+        }
+#pragma unroll
+        for (int q = 0; q < NI; q++) {
+            const int i = ii[q], j = jj[q], d = dv[q], u = d - 1;
+            if (!ok[q]) continue;
+            L.cc[off(d, N) + i - 1] = static_cast<uint8_t>(rtype(ty[q]) * 25 + (wjp[q] & 7) * 5 + (wim[q] & 7));
+            u32 h = INF16;
+            if (((wi1[q] >> 8) & 255) >= uint32_t(u)) {
+                h = padd(__float_as_uint(XS->hp[u]), f1[q]);
+                if (u == 3 || u == 4 || u == 6) {   // special hairpins (three diagonals)
+                    const uint32_t key = hp_key(L.S, i, u + 2);
+                    for (int q0 = 0; q0 < nsp; q0 += 8) {
+#pragma unroll
+                        for (int t = 0; t < 8; t++)
+                            if (spk[q0 + t] == key) h = spv[q0 + t];
+                    }
+                }
+            }
+            if (d == mL - 1 && mL > 0 && mt[q]) h = pmin(h, mextra);
+            if (inb[q]) {
+                L.qbm[off(d, N) + i - 1] = pr[q] ? h : MARK16;
+                L.qm1[colb(j) + i - 1] = pr[q] ? f2[q] : INF16;
+            }
+        }
+    };
+    for (int dd = 4 + wid; dd <= N - 1; dd += 2 * NWV) cell_pass(dd);
     __syncthreads();
 #ifdef ADX_STAMP
     const unsigned long long st_s4 = __builtin_amdgcn_s_memtime();   // per-cell pass
@@ -1052,6 +1112,12 @@ static hipError_t launch_pair_nm(const KArgs &ka, const uint8_t *seqs, int W, fl
         if (fa.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
         e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (e != hipSuccess) return e;
+        if (std::getenv("ADX_OCC")) {   // diagnostic: resident workgroups per CU at this LDS size
+            int nb = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(k), NWV * WAVE, lds);
+            std::fprintf(stderr, "mfe_pair_kernel<%d>: %d waves, %zu B LDS, %d VGPRs, %d workgroups per CU\n", NM,
+                         NWV, lds, fa.numRegs, nb);
+        }
         configured = true;
     }
     hipLaunchKernelGGL(k, dim3(W * ka.n_groups2), dim3(NWV * WAVE), lds, stream, ka, ka.X, ka.T, seqs, W, gout, mask);

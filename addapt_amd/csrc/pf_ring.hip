@@ -804,8 +804,12 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
         }
     } else {
         __builtin_amdgcn_s_setprio(2);
+        // one sweep instance per role (round 6, as pf_cells.hip): the shared loop
+        // kept every role's values live (65 SGPR spill reads / writes per step)
+        auto sweep = [&](auto role_c) __attribute__((always_inline)) {
+        constexpr int ROLE = decltype(role_c)::value;   // 0 M, 1 F, 2 Q, 3 R
         for (int s = 4; s <= s_end; s++) {
-            if (rg_mw(wid) >= 0) {
+            if constexpr (ROLE == 0) {
                 // ---------------- M: qm items of span sq = s - 2 (pf_cells.hip)
                 const int sq = s - 2;
                 if (sq >= 4 && sq <= N - 3) {
@@ -861,7 +865,7 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                     RSTAMP(6);
                     rload(s + 2, ph);   // in flight across the barrier
                 }
-            } else if (wid == RG_WF) {
+            } else if constexpr (ROLE == 1) {
                 vm_drain();        // last step's finalised cells (Q loads them this step)
                 // ---------------- F: the changed cells of diagonal e = s - 1
                 const int e = s - 1;
@@ -899,7 +903,7 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                         }
                     }
                 }
-            } else if (wid == RG_WQ) {
+            } else if constexpr (ROLE == 2) {
                 // ---------------- Q: q5[j], j = s - 3, from column j loaded last step
                 const int j = s - 3;
                 if (j >= 4 && j <= N && (!incr || j >= m_lo - 1)) {
@@ -931,7 +935,7 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                 // column s - 2 is final: its last cell, (1, s-2), was finalised two steps
                 // ago and its store drained by F at the start of the last step
                 qload(s - 2);
-            } else if (wid == RG_WR) {
+            } else {
                 vm_drain();        // last step's prep stores and loads (the record loads are a step old)
                 prep(s + 1, 2);
                 rload(s + 2, 2);
@@ -944,6 +948,11 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
             lds_barrier();
             RSTAMP(7);   // barrier
         }
+        };
+        if (rg_mw(wid) >= 0) sweep(std::integral_constant<int, 0>{});
+        else if (wid == RG_WF) sweep(std::integral_constant<int, 1>{});
+        else if (wid == RG_WQ) sweep(std::integral_constant<int, 2>{});
+        else sweep(std::integral_constant<int, 3>{});   // RG_WR
     }
     __syncthreads();
     RSTAMP(4);

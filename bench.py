@@ -424,6 +424,11 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
         "traffic_source": traffic_src,
         "kernel_ms_per_launch": kern_ms,
         "window_ms_per_launch": score_ms,
+        # since round 5 the per-variant score combine runs in step_tail_kernel,
+        # after the window's end event: the window is the step's fold launches
+        # (order_kernel, inside / outside folds, the MFE FP32-fallback scan) only
+        "window_note": "score window = order_kernel + fold launches (+ MFE fallback scan); "
+                       "excludes step_tail_kernel (accept, score combine, next proposal) since round 5",
         "inside_ms_per_launch": inside_ms,
         "outside_ms_per_launch": outside_ms if bppm else None,
         "inside_frac": ((scored_pl * flop_inside / (inside_ms * 1e-3) / 1e12) / peak
