@@ -515,12 +515,13 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
         L.qw[wo] = qbbm;
         L.ow[wo] = uint8_t((tp >> 8) & 255);
     };
-    auto fin = [&](int d) {
-        if (wid < 2) {
-            finalize(d, wid);
-        } else if (wid < 4) {
-            frec_write(d, wid - 2);   // diagonal d, finalized next step
-        } else if (wid == RW) {
+    auto fin = [&](int d, auto wc) {
+        constexpr int w = decltype(wc)::value;
+        if constexpr (w < 2) {
+            finalize(d, w);
+        } else if constexpr (w < 4) {
+            frec_write(d, w - 2);   // diagonal d, finalized next step
+        } else if (w == RW) {
             // setup records of diagonal d - 1 (next step's B) from the factors made last
             // step; the factors of diagonal d - 2, the rank list of d - 3
             rec_write(d - 1, pnext);
@@ -538,16 +539,16 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             // about the same time (stamps, tools/outside_stamps.py): the finalize
             // wave 0 one size and the record wave 7 none (a size >= 6 costs 3 reads for its
             // special shapes + one per 4 generic ones per lane-set, sizes <= 5 ~3 per shape)
-            case 0: b_sweep<2, 19, -1, -1, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 1: b_sweep<2, 5, 7, 15, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 2: b_sweep<2, 4, 0, 23, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 3: b_sweep<2, 3, 30, 6, 11, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 4: b_sweep<2, 29, 28, 27, 1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 5: b_sweep<2, 26, 25, 24, 2, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 6: b_sweep<2, 22, 21, 20, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 7: b_sweep<2, -1, -1, -1, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 8: b_sweep<2, 18, 17, 16, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            default: b_sweep<2, 14, 13, 12, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 0: b_sweep<2, 19, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 0>{}, fin OX_STP_ARGS); break;
+            case 1: b_sweep<2, 5, 7, 15, -1, -1>(L, N, lane, std::integral_constant<int, 1>{}, fin OX_STP_ARGS); break;
+            case 2: b_sweep<2, 4, 0, 23, -1, -1>(L, N, lane, std::integral_constant<int, 2>{}, fin OX_STP_ARGS); break;
+            case 3: b_sweep<2, 3, 30, 6, 11, -1>(L, N, lane, std::integral_constant<int, 3>{}, fin OX_STP_ARGS); break;
+            case 4: b_sweep<2, 29, 28, 27, 1, -1>(L, N, lane, std::integral_constant<int, 4>{}, fin OX_STP_ARGS); break;
+            case 5: b_sweep<2, 26, 25, 24, 2, -1>(L, N, lane, std::integral_constant<int, 5>{}, fin OX_STP_ARGS); break;
+            case 6: b_sweep<2, 22, 21, 20, 8, -1>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
+            case 7: b_sweep<2, -1, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;
+            case 8: b_sweep<2, 18, 17, 16, 10, -1>(L, N, lane, std::integral_constant<int, 8>{}, fin OX_STP_ARGS); break;
+            default: b_sweep<2, 14, 13, 12, 9, -1>(L, N, lane, std::integral_constant<int, 9>{}, fin OX_STP_ARGS); break;   // wave 9
         }
     } else for (int d = N - 1; d >= 3; d--) {
         const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d

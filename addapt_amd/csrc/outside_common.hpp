@@ -210,8 +210,10 @@ __device__ __forceinline__ float quad_sum_f(float v) {   // sum over the 4 lanes
 // (-1 = none), the block's shape factors held in registers for the whole sweep;
 // four lanes per inner cell (16 cells per lane-set; OxSizeQ), one barrier per
 // diagonal, as the M / F waves.
-template <int NSETS, int U0, int U1, int U2, int U3, int U4, class Fin>
-__device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, const Fin &fin OX_STP_PARAMS) {
+// wid: the wave as a compile-time constant (std::integral_constant; round 6), so
+// the role fin(d, wid) runs on this wave is resolved per instance
+template <int NSETS, int U0, int U1, int U2, int U3, int U4, class Fin, class Wid>
+__device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, Wid wid, const Fin &fin OX_STP_PARAMS) {
     constexpr auto tb = [](int u) { return u >= 2 && u <= 4; };
     constexpr bool TB = tb(U0) || tb(U1) || tb(U2) || tb(U3) || tb(U4);
     constexpr bool H5 = U0 == 5 || U1 == 5 || U2 == 5 || U3 == 5 || U4 == 5;   // 2x3 loops (m23)
@@ -267,7 +269,7 @@ __device__ __forceinline__ void b_sweep(const OxL &L, int N, int lane, int wid, 
             if (r == 0 && idx < ncell && (tp >> 16))   // the cell's natural slot (F reads lane = cell)
                 L.part[((par * NSETS + ((i - 1) >> 6)) * OX_NB + wid) * WAVE + ((i - 1) & (WAVE - 1))] = part;
         }
-        fin(d);   // F of diagonal d + 1 on waves 0 and 1
+        fin(d, wid);   // F of diagonal d + 1 on waves 0 and 1
         OSTAMP(5);
         lds_barrier();
         OSTAMP(6);   // barrier

@@ -630,12 +630,13 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
         }
         return acc + acc1;
     };
-    auto fin = [&](int d) {
-        if (wid < OR_SETS) {
-            finalize(d, wid);
-        } else if (wid < 2 * OR_SETS) {
-            frec_write(d, wid - OR_SETS);   // diagonal d, finalized next step
-        } else if (wid == RW) {
+    auto fin = [&](int d, auto wc) {
+        constexpr int w = decltype(wc)::value;
+        if constexpr (w < OR_SETS) {
+            finalize(d, w);
+        } else if constexpr (w < 2 * OR_SETS) {
+            frec_write(d, w - OR_SETS);   // diagonal d, finalized next step
+        } else if (w == RW) {
             rec_write(d - 1, pnext);
             pnext = tab_load(d - 2, inext);
             inext = idx_load(d - 3);
@@ -647,14 +648,14 @@ outside_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *s
             // loop sizes in blocks of about equal cost (a size >= 6: 3 reads for its
             // special shapes + one per 4 generic ones per lane-set; sizes <= 5 ~3 per
             // shape), a little less on the finalize (0-2) and record (7) waves
-            case 0: b_sweep<OR_SETS, 28, 20, 13, 0, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 1: b_sweep<OR_SETS, 27, 21, 1, 7, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 2: b_sweep<OR_SETS, 26, 22, 12, 6, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 3: b_sweep<OR_SETS, 4, 19, 14, -1, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 4: b_sweep<OR_SETS, 3, 24, 16, 9, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 5: b_sweep<OR_SETS, 30, 25, 18, 11, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            case 6: b_sweep<OR_SETS, 5, 23, 15, 8, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
-            default: b_sweep<OR_SETS, 29, 2, 17, 10, -1>(L, N, lane, wid, fin OX_STP_ARGS); break;
+            case 0: b_sweep<OR_SETS, 28, 20, 13, 0, -1>(L, N, lane, std::integral_constant<int, 0>{}, fin OX_STP_ARGS); break;
+            case 1: b_sweep<OR_SETS, 27, 21, 1, 7, -1>(L, N, lane, std::integral_constant<int, 1>{}, fin OX_STP_ARGS); break;
+            case 2: b_sweep<OR_SETS, 26, 22, 12, 6, -1>(L, N, lane, std::integral_constant<int, 2>{}, fin OX_STP_ARGS); break;
+            case 3: b_sweep<OR_SETS, 4, 19, 14, -1, -1>(L, N, lane, std::integral_constant<int, 3>{}, fin OX_STP_ARGS); break;
+            case 4: b_sweep<OR_SETS, 3, 24, 16, 9, -1>(L, N, lane, std::integral_constant<int, 4>{}, fin OX_STP_ARGS); break;
+            case 5: b_sweep<OR_SETS, 30, 25, 18, 11, -1>(L, N, lane, std::integral_constant<int, 5>{}, fin OX_STP_ARGS); break;
+            case 6: b_sweep<OR_SETS, 5, 23, 15, 8, -1>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
+            default: b_sweep<OR_SETS, 29, 2, 17, 10, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;   // wave 7
         }
     } else for (int d = N - 1; d >= 3; d--) {
         const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;
