@@ -58,14 +58,17 @@ namespace {
 #ifndef ADX_PAIR_NBLK
 #define ADX_PAIR_NBLK 7
 #endif
-constexpr int NWV = ADX_PAIR_NBLK + 1;
-constexpr int F_WAVE = NWV - 1;
+// eight waves; with ADX_PAIR_NBLK = 8 the finalize wave carries a block too (A/B)
+// (ten waves with nine blocks measured -37 %: a 10-wave workgroup's waves land
+// 3, 3, 2, 2 on the SIMDs, so a second one does not fit at 96 VGPRs)
+constexpr int NWV = 8;
+constexpr int F_WAVE = 7;
 constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
 
-#if ADX_PAIR_NBLK == 7
-#include "mfe_pair_blocks.inc"
+#if ADX_PAIR_NBLK == 8
+#include "mfe_pair_blocks8.inc"   // A/B: eight block waves (ADX_GEN_PAIR_NBLK=8)
 #else
-#include "mfe_pair_blocks9.inc"   // A/B: nine block waves (ADX_GEN_PAIR_NBLK=9)
+#include "mfe_pair_blocks.inc"
 #endif
 static_assert(MFE_NBLK == ADX_PAIR_NBLK, "one block per block wave");
 
