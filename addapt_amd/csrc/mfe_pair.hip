@@ -58,18 +58,15 @@ namespace {
 #ifndef ADX_PAIR_NBLK
 #define ADX_PAIR_NBLK 7
 #endif
-// eight waves; with ADX_PAIR_NBLK = 8 the finalize wave carries a block too (A/B)
-// (ten waves with nine blocks measured -37 %: a 10-wave workgroup's waves land
-// 3, 3, 2, 2 on the SIMDs, so a second one does not fit at 96 VGPRs)
+// eight waves (ten waves with nine blocks measured -37 %: a 10-wave workgroup's
+// waves land 3, 3, 2, 2 on the SIMDs, so a second one does not fit at 96 VGPRs)
 constexpr int NWV = 8;
 constexpr int F_WAVE = 7;
 constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
 
-#if ADX_PAIR_NBLK == 8
-#include "mfe_pair_blocks8.inc"   // A/B: eight block waves (ADX_GEN_PAIR_NBLK=8)
-#else
+// (A/B round 6: a block on the finalize wave too, ADX_GEN_PAIR_NBLK=8, measured
+// -5.7 %: the finalize wave then sets the step; nine block waves in ten -37 %)
 #include "mfe_pair_blocks.inc"
-#endif
 static_assert(MFE_NBLK == ADX_PAIR_NBLK, "one block per block wave");
 
 constexpr int PINF = 32767;   // an impossible half, sign-extended (the partial slots)

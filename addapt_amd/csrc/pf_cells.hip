@@ -39,20 +39,21 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #ifndef PX_NMW_CFG
 #define PX_NMW_CFG 4
 #endif
-constexpr int PX_NB = 7;              // interior-loop blocks (waves 0..6)
-constexpr int PX_NMW = PX_NMW_CFG;    // qm item waves (10 .. 10 + PX_NMW - 1)
-constexpr int PX_NW = 10 + PX_NMW;
+#ifndef PX_NB_CFG
+#define PX_NB_CFG 7
+#endif
+constexpr int PX_NB = PX_NB_CFG;      // interior-loop blocks (waves 0 .. PX_NB - 1)
+constexpr int PX_NMW = PX_NMW_CFG;    // qm item waves (PX_NB + 3 .. PX_NB + 2 + PX_NMW)
+constexpr int PX_M0 = PX_NB + 3;
+constexpr int PX_NW = PX_M0 + PX_NMW;
 constexpr int PX_NT = PX_NW * WAVE;
-// Roles of waves 7-13 (seven interior-loop waves, four qm waves: the qm wave
+// Roles of the waves after the blocks (F, Q, R, then four qm waves: the qm wave
 // with the most items sets the step at a power-of-two lane split, so a fourth
 // qm wave halves it at about half of the spans; measured +1 % over 8 + 3).
-#ifndef PX_ROLES
-#define PX_ROLES 7, 8, 9
-#endif
-constexpr int PX_ROLE_W[3] = {PX_ROLES};
-constexpr int PX_WF = PX_ROLE_W[0], PX_WQ = PX_ROLE_W[1], PX_WR = PX_ROLE_W[2];   // F, Q, R
+constexpr int PX_WF = PX_NB, PX_WQ = PX_NB + 1, PX_WR = PX_NB + 2;   // F, Q, R
 __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most items) or -1
-    return w == 10 ? 0 : w == 11 ? 1 : w == 13 ? 2 : w == 12 ? 3 : (w >= 14 && w < PX_NW) ? w - 10 : -1;
+    return w == PX_M0 ? 0 : w == PX_M0 + 1 ? 1 : w == PX_M0 + 3 ? 2 : w == PX_M0 + 2 ? 3
+         : (w >= PX_M0 + 4 && w < PX_NW) ? w - PX_M0 : -1;
 }
 constexpr int PX_NMAX = 100;
 constexpr int PX_RF = 8;              // record fields (rec_store): word, mmo, mo, m23, 1x1..2x2 factors
@@ -85,7 +86,7 @@ __device__ __forceinline__ f2 dpp_add2(f2 v) {
 
 struct PxLay {
     int C, NP;
-    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, UC, Q5, CT, DT, PW, BY, MT, BYTES;
+    size_t QB, QM, Q1, CC, PART, REC, CL, MLA, UC, Q5, CT, DT, PW, BY, MT, FL, BYTES;
     __host__ __device__ static size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
     __host__ __device__ explicit PxLay(int N) {
         C = ((N - 4) * (N - 3)) / 2;
@@ -102,10 +103,11 @@ struct PxLay {
         UC = o;   o += a16(size_t(2) * NP * 8);                   // unpaired part U(i, j) of qm by column j, by span parity
         Q5 = o;   o += a16(size_t(NP) * 8);
         CT = o;   o += a16(size_t(CT_SIZE) * 4);
-        DT = o;   o += a16(size_t(DT_HP + N + 1) * 4);
+        DT = o;   o += a16(size_t(DT_HP) * 4);                    // (hairpin lengths: XS->hp, scalar loads)
         PW = o;   o += a16(size_t(N + 9) * 4);                    // (expMLbase sigma)^t
         BY = o;   o += a16(size_t(7) * NP);                       // S, up, dn, ptn, enc, flg, mat
         MT = o;   o += a16(size_t(MAX_SPECIAL_HP) * 8 + 2 * MAX_MOTIF);   // special hairpins, motif codes / partners
+        FL = o;   o += 16;                                        // block_or word
         BYTES = o;
     }
 };
@@ -514,6 +516,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         }
     }
     const bool incr = src != nullptr;
+    if (tid == 0) *reinterpret_cast<int *>(smem + Y.FL) = 0;   // block_or word (read after two barriers)
     m_lo = uni(m_lo);
     m_hi = uni(m_hi);
     auto clo = [&](int D) { return incr ? max(1, m_lo - 1 - D) : 1; };
@@ -581,7 +584,6 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     }
     for (int k = tid; k < 288; k += PX_NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
     for (int k = tid; k < 8; k += PX_NT) L.dt[DT_TAU + k] = T.termAU[k];
-    for (int k = tid; k <= N; k += PX_NT) L.dt[DT_HP + k] = XS->hp[k];
     for (int k = tid; k < N + 9; k += PX_NT) L.pw[k] = XS->pwml[k];
     for (int k = tid; k < MAX_SPECIAL_HP; k += PX_NT) {
         const bool on = k < XS->n_special;
@@ -594,7 +596,8 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     }
     for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
     for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
-    const bool constrained = __syncthreads_or(cst);
+    __syncthreads();   // orders tid 0's zeroing of the block_or word before the ORs
+    const bool constrained = block_or(reinterpret_cast<int *>(smem + Y.FL), cst);
     PSTAMP(1);
     if (tid == 0) {   // ViennaRNA's S1 wrap-around
         L.S[0] = L.S[N];
@@ -685,7 +688,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                                 }
                             }
                             if (!special)
-                                h = L.dt[DT_HP + u] * ((u == 3) ? L.dt[DT_TAU + type]
+                                h = XS->hp[u] * ((u == 3) ? L.dt[DT_TAU + type]
                                                                 : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
                         }
                         const bool mx = D == mL - 1 && mL > 0 && L.mat[i];
@@ -846,6 +849,20 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     if (wid == PX_WQ) qfac(4);
     const int s_end = N + 1;
     if (wid < PX_NB) {
+#if PX_NB_CFG == 8
+        // eight blocks (A/B, round 6): sizes 9, 14, 6, 13 of the four blocks the
+        // stamps showed busiest (profiles/r06e_pf_cells_stamps.txt) on an eighth wave
+        switch (wid) {
+            case 0: pb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 1: pb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 2: pb_sweep<3, 20, 18, 8, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<28, 26, 1, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 16, 0, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            default: pb_sweep<9, 14, 6, 13, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+        }
+#else
         switch (wid) {
             // blocks of about equal LDS cost per lane-set (a size >= 6: 3 reads for
             // its special shapes + one per 4 generic ones; the small sizes ~3 per shape)
@@ -859,6 +876,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             default: pb_sweep<24, 25, 23, 15, 13>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
         }
+#endif
     } else {
         // the M / F / Q / R chains set the step time; issue arbitration favours the
         // older (B) waves of the workgroup, so these run at a higher priority
@@ -1036,8 +1054,8 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
 // LDS bytes of the lanes = cells PF kernel for this workload (0: not covered)
 size_t pf_cells_lds(const KArgs &ka) {
     if (ka.mode != 0 || ka.Nmax > PX_NMAX || ka.Nmax < 8) return 0;
-    const size_t b = PxLay(ka.Nmax).BYTES;
-    return b + 256 <= 160 * 1024 ? b : 0;
+    const size_t b = PxLay(ka.Nmax).BYTES;   // no static LDS (block_or, not __syncthreads_or)
+    return b <= 160 * 1024 ? b : 0;
 }
 
 hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const int *mask, float *gout,
