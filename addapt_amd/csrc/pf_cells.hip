@@ -40,7 +40,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define PX_NMW_CFG 4
 #endif
 #ifndef PX_NB_CFG
-#define PX_NB_CFG 7
+#define PX_NB_CFG 8   // eight interior-loop waves (round 6: +1.2 % PF over seven, A/B r06f)
 #endif
 constexpr int PX_NB = PX_NB_CFG;      // interior-loop blocks (waves 0 .. PX_NB - 1)
 constexpr int PX_NMW = PX_NMW_CFG;    // qm item waves (PX_NB + 3 .. PX_NB + 2 + PX_NMW)
