@@ -582,6 +582,10 @@ struct Problem {
     // configuration (P = 2 value arrays, one group per variant)
     adx_status alloc_state(int W) {
         tab_slot = size_t(variants.size()) * inc_group_floats(kargs().cells, Nmax, 2);
+        // the MFE16 slots' per-cell codes follow the groups' tables (dev_types.hpp)
+        const int ng = int((variants.size() + 1) / 2) + int(variants.size());
+        tab_slot = std::max(tab_slot, inc_cc_offset(kargs().cells, Nmax, ng, ng));
+        tab_slot = (tab_slot + 3) / 4 * 4;   // 16-byte aligned slots (the codes are read as uint4)
         HIP_TRY(dTab.alloc(size_t(W) * 2 * tab_slot));
         HIP_TRY(dCur.alloc(W));
         HIP_TRY(dValid.alloc(W));

@@ -134,6 +134,14 @@ __host__ __device__ inline uint32_t hp_key(const uint8_t *S, int i, int len) {
 __host__ __device__ inline size_t inc_group_floats(int cells, int Nmax, int P) {
     return size_t(P) * (3 * size_t(cells) + size_t(Nmax) + 2);
 }
+// MFE (packed 16-bit) slots also keep every cell's inner-pair code (one byte per
+// cell, 16-byte aligned, after the n_groups2 groups' value arrays), so a refold
+// restores the codes with the tables and recomputes only its band's
+// (mfe_pair.hip; every MFE16 kernel writes them)
+__host__ __device__ inline size_t inc_cc_floats(int cells) { return (size_t(cells) + 15) / 16 * 4; }
+__host__ __device__ inline size_t inc_cc_offset(int cells, int Nmax, int n_groups2, int g) {
+    return (size_t(n_groups2) * inc_group_floats(cells, Nmax, 1) + 3) / 4 * 4 + size_t(g) * inc_cc_floats(cells);
+}
 
 struct KArgs {
     const DevTables *T;

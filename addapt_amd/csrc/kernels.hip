@@ -530,6 +530,7 @@ struct Inc {
     const float *src;
     float *dst;
     int m_lo, m_hi;
+    uint8_t *cc_dst;   // MinPlus16: the slot's per-cell codes (dev_types.hpp inc_cc_offset)
 };
 
 template <int NT, int P, class SR>
@@ -1130,6 +1131,8 @@ __device__ void pf_group(const KArgs &ka, const int *vs, const uint8_t *raw, con
             }
             for (int k = tid; k <= N; k += NT) dp[3 * C + k] = L.q5[p][k];
         }
+        if (inc.cc_dst)   // MinPlus16: the codes too (mfe_pair.hip restores them)
+            for (int k = tid; k < int(C); k += NT) inc.cc_dst[k] = k < ((N - 4) * (N - 3)) / 2 ? L.cc[k] : 0;
     }
     bad = false;
     if constexpr (SR::NV == 2) {
@@ -1195,12 +1198,15 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
         }
         float z[P];
         bool bad = false;
-        Inc inc{nullptr, nullptr, 0, 0};
+        Inc inc{nullptr, nullptr, 0, 0, nullptr};
         if (ka.tab) {   // MC state: read the current tables, write this proposal's
             const size_t G = inc_group_floats(ka.cells, ka.Nmax, P);
             const int cur = ka.cur_slot[w];
             float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
             inc.dst = base + size_t(1 - cur) * ka.tab_slot + size_t(g) * G;
+            if constexpr (P == 1 && SR::NV == 2)
+                inc.cc_dst = reinterpret_cast<uint8_t *>(base + size_t(1 - cur) * ka.tab_slot +
+                                                         inc_cc_offset(ka.cells, ka.Nmax, ka.n_groups2, g));
             if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
                 const int lb = ka.variants[vs[0]].before_len;
                 inc.src = base + size_t(cur) * ka.tab_slot + size_t(g) * G;
@@ -1702,7 +1708,7 @@ bppm_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int
     const int vs[1] = {v};
     float z[1];
     bool bad = false;
-    Inc inc{nullptr, nullptr, 0, 0};
+    Inc inc{nullptr, nullptr, 0, 0, nullptr};
     if (reuse && ka.tab) {
         const size_t B = 3 * size_t(ka.cells) + size_t(ka.Nmax) + 2;   // one variant's tables
         // score P = 1: group = variant; P = 2: the groups2 position (host-computed)

@@ -165,6 +165,8 @@ struct IncM {
     const u32 *src;
     u32 *dst;
     int m_lo, m_hi;
+    const uint4 *cc_src;   // the slots' per-cell codes (dev_types.hpp inc_cc_offset)
+    uint4 *cc_dst;
 };
 
 __device__ __forceinline__ int lanesets(int n) { return (n + 63) >> 6; }
@@ -206,6 +208,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     constexpr int RS = (3 * (CNM >> 1) + NT - 1) / NT;   // loads per thread
     const int Crs = ((N - 4) * (N - 3)) >> 1, half = Crs >> 1;
     uint2 rsv[RS];
+    constexpr int RC = (((CNM + 15) >> 4) + NT - 1) / NT;   // per-cell code loads per thread (uint4)
+    const int C16 = (Crs + 15) >> 4;
+    uint4 rcv[RC];
     if (incr) {
         const size_t Cs = size_t(ka.cells);
 #pragma unroll
@@ -214,6 +219,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             const int kk = k < 3 * half ? k : 0;
             const int a = kk / half, c = kk - a * half;
             rsv[t] = *reinterpret_cast<const uint2 *>(inc.src + a * Cs + 2 * c);
+        }
+#pragma unroll
+        for (int t = 0; t < RC; t++) {
+            const int k = tid + t * NT;
+            rcv[t] = inc.cc_src[k < C16 ? k : 0];
         }
     }
     // setup scratch in the partial / split / U slots (first written after the per-cell pass)
@@ -328,6 +338,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         }
         if (Crs & 1)
             for (int a = tid; a < 3; a += NT) (a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1)[Crs - 1] = inc.src[a * Cs + Crs - 1];
+#pragma unroll
+        for (int t = 0; t < RC; t++) {   // the codes (16 cells per store; the band's are recomputed)
+            const int k = tid + t * NT;
+            if (k < C16) reinterpret_cast<uint4 *>(L.cc)[k] = rcv[t];
+        }
         for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) L.q5[k] = inc.src[3 * Cs + k];
     }
     __syncthreads();
@@ -357,9 +372,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
 #pragma unroll
         for (int q = 0; q < NI; q++) {
             const int d = dd0 + (q >> 1) * NWV;
-            const int r = lane + (q & 1) * WAVE;
+            // the changed band's rows (a fold from scratch: every row); a refold
+            // restored the other cells' codes, tables and marks
+            const int r = clo(d) - 1 + lane + (q & 1) * WAVE;
             dv[q] = d;
-            ok[q] = d <= N - 1 && r < N - d;
+            ok[q] = d <= N - 1 && r < chi(d);
             const int i = ok[q] ? r + 1 : 1, j = ok[q] ? i + d : 5;
             ii[q] = i;
             jj[q] = j;
@@ -379,7 +396,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             const int i = ii[q], j = jj[q], d = dv[q];
             const int si = wi[q] & 7, sj = wj[q] & 7;
             ty[q] = ptype(si, sj);
-            inb[q] = ok[q] && i >= clo(d) && i <= chi(d);
+            inb[q] = ok[q];
             const int fi = (wi[q] >> 3) & 7, fj = (wj[q] >> 3) & 7;
             const int pi = (wi[q] >> 16) & 255, pj = (wj[q] >> 16) & 255;
             bool al = !((fi | fj) & 1) && !((fi & 2) || (fj & 4));
@@ -1008,6 +1025,8 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             dp[2 * C + k] = L.qm1[k];
         }
         for (int k = tid; k <= N; k += NT) dp[3 * C + k] = L.q5[k];
+        const int C16 = (((N - 4) * (N - 3)) / 2 + 15) >> 4;
+        for (int k = tid; k < C16; k += NT) inc.cc_dst[k] = reinterpret_cast<const uint4 *>(L.cc)[k];
     }
     bool low = false;
     const int C = ((N - 4) * (N - 3)) >> 1;
@@ -1065,17 +1084,20 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     }
     __syncthreads();
     const int vs[2] = {ka.groups2[2 * g], ka.groups2[2 * g + 1]};
-    IncM inc{nullptr, nullptr, 0, 0};
+    IncM inc{nullptr, nullptr, 0, 0, nullptr, nullptr};
     if (ka.tab) {
         const size_t Gf = inc_group_floats(ka.cells, ka.Nmax, 1);
         const int cur = ka.cur_slot[w];
         float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
         inc.dst = reinterpret_cast<u32 *>(base + size_t(1 - cur) * ka.tab_slot + size_t(g) * Gf);
+        const size_t cco = inc_cc_offset(ka.cells, ka.Nmax, ng, g);
+        inc.cc_dst = reinterpret_cast<uint4 *>(base + size_t(1 - cur) * ka.tab_slot + cco);
         // a sibling group may clear tab_valid[w] on overflow while this one reads it:
         // either value is correct (an incremental refold equals a fold from scratch)
         if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
             const int lb = ka.variants[vs[0]].before_len;
             inc.src = reinterpret_cast<const u32 *>(base + size_t(cur) * ka.tab_slot + size_t(g) * Gf);
+            inc.cc_src = reinterpret_cast<const uint4 *>(base + size_t(cur) * ka.tab_slot + cco);
             inc.m_lo = ka.chg[2 * w] + 1 + lb;
             inc.m_hi = ka.chg[2 * w + 1] + 1 + lb;
         }
