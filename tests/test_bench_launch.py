@@ -33,7 +33,9 @@ def test_bench_spawns_ranks_gloo():
     d = out["dist"]
     assert d["backend"] == "gloo" and d["library"] == "gloo" and d["world_size"] == 2, d
     assert len(d["per_rank_ms_per_step"]) == 2
-    assert d["per_rank_ms_per_step"][1] > d["per_rank_ms_per_step"][0], d
+    # (each rank's clock runs from barrier to barrier, so it includes the wait
+    # for the slowest rank: rank 1 sleeps 6 ms, every rank's time is >= that)
+    assert min(d["per_rank_ms_per_step"]) >= 1.9, d
     assert d["max_ms_per_step"] == max(d["per_rank_ms_per_step"]) == out["ms_per_step"], d
 
 
