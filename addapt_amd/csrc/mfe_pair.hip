@@ -819,8 +819,13 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     if (sh >= 1) acc = fold_halves(acc);
                     if (r == 0) {
                         int *pp = L.part + (dd & 3) * 2 * NP + i;
+#ifndef ADX_ABL_NOATOM
                         atomicMin(pp, sext_lo(acc));
                         atomicMin(pp + NP, sext_hi(acc));
+#else   // diagnostic (results wrong): plain stores instead of the atomic minima
+                        pp[0] = sext_lo(acc);
+                        pp[NP] = sext_hi(acc);
+#endif
                     }
                 }
             }
@@ -830,7 +835,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         // ---------------- M: split parts of qm for spans d and d+1 (lanes = cells x
         // slices of the split points, mfe_cells.hip): min over t >= 5 of
         // qm(i, i+t-1) + qm1(i+t, j), written to the span's slot for F
+#ifndef ADX_ABL_NOM
         if (wid == mw[0] || wid == mw[1]) {
+#else   // diagnostic (results wrong): no split parts
+        if (false) {
+#endif
             __builtin_amdgcn_s_setprio(PRIO_ROLE);
             {
                 const int s = wid == mw[0] ? d : d + 1;

@@ -398,6 +398,8 @@ def measure(a, fold, bppm, length, steps, warmup, rank, world, gids_rank, dist, 
     # (3 cell tables + q5) x 4 B
     cells = (length - 4) * (length - 3) // 2
     state_bytes = 2 * (1 if fold == "mfe" else 2) * (3 * cells + length + 2) * 4
+    if fold == "mfe":   # round 6: MFE slots also keep each cell's inner-pair code (1 B)
+        state_bytes += 2 * ((cells + 15) // 16) * 16
     traffic, traffic_src = _traffic(traffic_json, fold, bppm, length, kern_name)
     peak, peak_note = roofline.valu_peak(fold)
     roof = {
