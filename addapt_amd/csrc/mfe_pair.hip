@@ -66,11 +66,7 @@ constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block
 
 // (A/B round 6: a block on the finalize wave too, ADX_GEN_PAIR_NBLK=8, measured
 // -5.7 %: the finalize wave then sets the step; nine block waves in ten -37 %)
-#if ADX_PAIR_QWAVE == 7
-#include "mfe_pair_blocks_q7.inc"   // A/B: the partition without wave 3's q5 seed
-#else
 #include "mfe_pair_blocks.inc"
-#endif
 static_assert(MFE_NBLK == ADX_PAIR_NBLK, "one block per block wave");
 
 constexpr int PINF = 32767;   // an impossible half, sign-extended (the partial slots)
@@ -468,11 +464,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     U.N = N;
     const uint32_t aqm = lds_addr(L.qm), aqm1 = lds_addr(L.qm1), ae4 = lds_addr(L.e4);
     constexpr int L_WAVE = 1;           // (round 5: wave 1 +0.8 % over wave 4, A/B r05zn/r05zo) the lists two steps ahead (diagonals d+4, d+5) and their B records
-#ifndef ADX_PAIR_QWAVE
-#define ADX_PAIR_QWAVE 3
-#endif
-    constexpr int Q_WAVE = ADX_PAIR_QWAVE;   // q5 of two columns (A/B: 7, the finalize wave, which waits
-                                             // 131 k cycles per group at the barrier; r06h stamps)
+    constexpr int Q_WAVE = 3;           // q5 of two columns (on the finalize wave: -2.1 %, A/B r06n)
     constexpr int fw[2] = {F_WAVE, 6};  // finalize lane-sets 0, 1 (rows 1..64, 64..127): lane-set 1
                                         // (spans < 38) rides on block wave 6
     constexpr int mw[2] = {0, 2};       // the split parts of spans d, d+1
