@@ -174,91 +174,6 @@ __device__ __forceinline__ int sext_lo(u32 x) { return int(short(x & 0xFFFFu)); 
 __device__ __forceinline__ int sext_hi(u32 x) { return int(x) >> 16; }
 __device__ __forceinline__ u32 pack2(int lo, int hi) { return (u32(lo) & 0xFFFFu) | (u32(hi) << 16); }
 
-// The split parts' reads with the split points interleaved over a cell's S
-// lanes (element k at t0 + S k: the cell's lanes read consecutive words of its
-// qm row and qm1 column); one LDS round trip per chunk (mfe_pair_fold M)
-template <int NR, int S>
-__device__ __forceinline__ void m_reads(u32 (&av)[NR], u32 (&rv)[NR], uint32_t pa, uint32_t pr) {
-    static_assert(NR == 4 || NR == 8 || NR == 16, "chunk sizes");
-    if constexpr (NR == 16) {
-        asm volatile(
-            "ds_read_b32 %0, %[pa] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %1, %[pa] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %2, %[pa] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %3, %[pa] offset:(3*4*%c[s])\n"
-            "ds_read_b32 %4, %[pa] offset:(4*4*%c[s])\n"
-            "ds_read_b32 %5, %[pa] offset:(5*4*%c[s])\n"
-            "ds_read_b32 %6, %[pa] offset:(6*4*%c[s])\n"
-            "ds_read_b32 %7, %[pa] offset:(7*4*%c[s])\n"
-            "ds_read_b32 %8, %[pa] offset:(8*4*%c[s])\n"
-            "ds_read_b32 %9, %[pa] offset:(9*4*%c[s])\n"
-            "ds_read_b32 %10, %[pa] offset:(10*4*%c[s])\n"
-            "ds_read_b32 %11, %[pa] offset:(11*4*%c[s])\n"
-            "ds_read_b32 %12, %[pa] offset:(12*4*%c[s])\n"
-            "ds_read_b32 %13, %[pa] offset:(13*4*%c[s])\n"
-            "ds_read_b32 %14, %[pa] offset:(14*4*%c[s])\n"
-            "ds_read_b32 %15, %[pa] offset:(15*4*%c[s])\n"
-            "ds_read_b32 %16, %[pr] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %17, %[pr] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %18, %[pr] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %19, %[pr] offset:(3*4*%c[s])\n"
-            "ds_read_b32 %20, %[pr] offset:(4*4*%c[s])\n"
-            "ds_read_b32 %21, %[pr] offset:(5*4*%c[s])\n"
-            "ds_read_b32 %22, %[pr] offset:(6*4*%c[s])\n"
-            "ds_read_b32 %23, %[pr] offset:(7*4*%c[s])\n"
-            "ds_read_b32 %24, %[pr] offset:(8*4*%c[s])\n"
-            "ds_read_b32 %25, %[pr] offset:(9*4*%c[s])\n"
-            "ds_read_b32 %26, %[pr] offset:(10*4*%c[s])\n"
-            "ds_read_b32 %27, %[pr] offset:(11*4*%c[s])\n"
-            "ds_read_b32 %28, %[pr] offset:(12*4*%c[s])\n"
-            "ds_read_b32 %29, %[pr] offset:(13*4*%c[s])\n"
-            "ds_read_b32 %30, %[pr] offset:(14*4*%c[s])\n"
-            "ds_read_b32 %31, %[pr] offset:(15*4*%c[s])\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(av[6]), "=&v"(av[7]), "=&v"(av[8]), "=&v"(av[9]), "=&v"(av[10]), "=&v"(av[11]), "=&v"(av[12]), "=&v"(av[13]), "=&v"(av[14]), "=&v"(av[15]), "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3]), "=&v"(rv[4]), "=&v"(rv[5]), "=&v"(rv[6]), "=&v"(rv[7]), "=&v"(rv[8]), "=&v"(rv[9]), "=&v"(rv[10]), "=&v"(rv[11]), "=&v"(rv[12]), "=&v"(rv[13]), "=&v"(rv[14]), "=&v"(rv[15])
-            : [pa] "v"(pa), [pr] "v"(pr), [s] "i"(S)
-            : "memory");
-    }
-    if constexpr (NR == 8) {
-        asm volatile(
-            "ds_read_b32 %0, %[pa] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %1, %[pa] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %2, %[pa] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %3, %[pa] offset:(3*4*%c[s])\n"
-            "ds_read_b32 %4, %[pa] offset:(4*4*%c[s])\n"
-            "ds_read_b32 %5, %[pa] offset:(5*4*%c[s])\n"
-            "ds_read_b32 %6, %[pa] offset:(6*4*%c[s])\n"
-            "ds_read_b32 %7, %[pa] offset:(7*4*%c[s])\n"
-            "ds_read_b32 %8, %[pr] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %9, %[pr] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %10, %[pr] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %11, %[pr] offset:(3*4*%c[s])\n"
-            "ds_read_b32 %12, %[pr] offset:(4*4*%c[s])\n"
-            "ds_read_b32 %13, %[pr] offset:(5*4*%c[s])\n"
-            "ds_read_b32 %14, %[pr] offset:(6*4*%c[s])\n"
-            "ds_read_b32 %15, %[pr] offset:(7*4*%c[s])\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(av[6]), "=&v"(av[7]), "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3]), "=&v"(rv[4]), "=&v"(rv[5]), "=&v"(rv[6]), "=&v"(rv[7])
-            : [pa] "v"(pa), [pr] "v"(pr), [s] "i"(S)
-            : "memory");
-    }
-    if constexpr (NR == 4) {
-        asm volatile(
-            "ds_read_b32 %0, %[pa] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %1, %[pa] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %2, %[pa] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %3, %[pa] offset:(3*4*%c[s])\n"
-            "ds_read_b32 %4, %[pr] offset:(0*4*%c[s])\n"
-            "ds_read_b32 %5, %[pr] offset:(1*4*%c[s])\n"
-            "ds_read_b32 %6, %[pr] offset:(2*4*%c[s])\n"
-            "ds_read_b32 %7, %[pr] offset:(3*4*%c[s])\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(rv[0]), "=&v"(rv[1]), "=&v"(rv[2]), "=&v"(rv[3])
-            : [pa] "v"(pa), [pr] "v"(pr), [s] "i"(S)
-            : "memory");
-    }
-}
-
 // One instance per wave (WID): every wave's sweep holds only its own interior-loop
 // block and roles, so the registers of the other waves' roles are not live in it
 template <int NT, int NM, int WID>
@@ -933,68 +848,6 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                 const int Lm = lanesets(hi - lo + 1);
                 const int Tt = s - 4;
                 u32 *slot = L.mla + (s % 6) * NP;
-#ifdef ADX_M_INTERLEAVE
-                for (int ls = 0; ls < Lm; ls++) {
-                    // lanes = cells x slices, cell-major (a cell's S = 2^lsl slices on
-                    // consecutive lanes); slice rr takes the split points t = 5 + rr + S m,
-                    // so a cell's lanes read consecutive words (round 6: the contiguous runs
-                    // per lane conflicted on ~48 % of M's LDS cycles, r06m)
-                    const int nc = min(WAVE, hi - lo + 1 - ls * WAVE);
-                    const int lc = nc <= 1 ? 0 : 32 - __clz(nc - 1);
-                    const int lsl = 6 - lc;
-                    const int c = lane >> lsl, rr = lane & ((1 << lsl) - 1);
-                    int i = lo + ls * WAVE + c;
-                    const bool valid = c < nc;
-                    if (!valid) i = hi;
-                    const int j = i + s;
-                    const int nb = Tt - 4;                                  // split points t = 5..Tt
-                    const int bs = nb > 0 ? (nb + (1 << lsl) - 1) >> lsl : 0;   // per lane
-                    u32 sp0 = INF16, sp1 = INF16;
-                    auto run = [&](auto sc) __attribute__((always_inline)) {
-                        constexpr int S = decltype(sc)::value;
-                        constexpr int LS = S == 1 ? 0 : S == 2 ? 1 : S == 4 ? 2 : S == 8 ? 3 : S == 16 ? 4 : S == 32 ? 5 : 6;
-                        auto chunk = [&](auto nconst, int m0) __attribute__((always_inline)) {
-                            constexpr int NR = decltype(nconst)::value;
-                            const int t0 = 5 + rr + S * m0;
-                            u32 av[NR], rv[NR];
-                            m_reads<NR, S>(av, rv, aqm1 + uint32_t(colb(j) + i - 1 + t0) * 4u,
-                                           aqm + uint32_t(rowb(i, N) - 5 + t0) * 4u);
-                            const int limk = (Tt - t0) >> LS;   // elements k <= limk are split points
-                            if (__ballot(limk < NR - 1) == 0) {
-#pragma unroll
-                                for (int k = 0; k < NR; k += 2) {
-                                    sp0 = pmin(sp0, padd(rv[k], av[k]));
-                                    sp1 = pmin(sp1, padd(rv[k + 1], av[k + 1]));
-                                }
-                            } else {
-#pragma unroll
-                                for (int k = 0; k < NR; k += 2) {
-                                    sp0 = pmin(sp0, padd(rv[k], k <= limk ? av[k] : INF16));
-                                    sp1 = pmin(sp1, padd(rv[k + 1], k + 1 <= limk ? av[k + 1] : INF16));
-                                }
-                            }
-                        };
-                        int m0 = 0;
-                        for (int ch = 0; ch < (bs >> 4); ch++, m0 += 16) chunk(std::integral_constant<int, 16>{}, m0);
-                        const int rem = bs & 15;
-                        if (rem > 8) chunk(std::integral_constant<int, 16>{}, m0);
-                        else if (rem > 4) chunk(std::integral_constant<int, 8>{}, m0);
-                        else if (rem > 0) chunk(std::integral_constant<int, 4>{}, m0);
-                    };
-                    switch (lsl) {
-                        case 0: run(std::integral_constant<int, 1>{}); break;
-                        case 1: run(std::integral_constant<int, 2>{}); break;
-                        case 2: run(std::integral_constant<int, 4>{}); break;
-                        case 3: run(std::integral_constant<int, 8>{}); break;
-                        case 4: run(std::integral_constant<int, 16>{}); break;
-                        case 5: run(std::integral_constant<int, 32>{}); break;
-                        default: run(std::integral_constant<int, 64>{}); break;
-                    }
-                    u32 split = pmin(sp0, sp1);
-                    for (int k = 1; k < (1 << lsl); k <<= 1) split = pmin(split, u32(__shfl_xor(int(split), k, WAVE)));
-                    if (valid && rr == 0) slot[i] = pfin(split);
-                }
-#else
                 for (int ls = 0; ls < Lm; ls++) {
                     const int nc = min(WAVE, hi - lo + 1 - ls * WAVE);
                     const int lc = nc <= 1 ? 0 : 32 - __clz(nc - 1);
@@ -1117,7 +970,6 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     for (int k = cst; k < WAVE; k <<= 1) split = pmin(split, u32(__shfl_xor(int(split), k, WAVE)));
                     if (valid && rr == 0) slot[i] = pfin(split);
                 }
-#endif
                 }
             }
             __builtin_amdgcn_s_setprio(0);
