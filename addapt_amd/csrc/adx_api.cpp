@@ -585,6 +585,7 @@ struct Problem {
         // the MFE16 slots' per-cell codes follow the groups' tables (dev_types.hpp)
         const int ng = int((variants.size() + 1) / 2) + int(variants.size());
         tab_slot = std::max(tab_slot, inc_cc_offset(kargs().cells, Nmax, ng, ng));
+        tab_slot = std::max(tab_slot, inc_cc_offset_pf(kargs().cells, Nmax, ng, ng));
         tab_slot = (tab_slot + 3) / 4 * 4;   // 16-byte aligned slots (the codes are read as uint4)
         HIP_TRY(dTab.alloc(size_t(W) * 2 * tab_slot));
         HIP_TRY(dCur.alloc(W));

@@ -142,6 +142,10 @@ __host__ __device__ inline size_t inc_cc_floats(int cells) { return (size_t(cell
 __host__ __device__ inline size_t inc_cc_offset(int cells, int Nmax, int n_groups2, int g) {
     return (size_t(n_groups2) * inc_group_floats(cells, Nmax, 1) + 3) / 4 * 4 + size_t(g) * inc_cc_floats(cells);
 }
+// the same for the PF slots (two value arrays per group: pf_cells.hip, kernels.hip SumProd)
+__host__ __device__ inline size_t inc_cc_offset_pf(int cells, int Nmax, int n_groups2, int g) {
+    return (size_t(n_groups2) * inc_group_floats(cells, Nmax, 2) + 3) / 4 * 4 + size_t(g) * inc_cc_floats(cells);
+}
 
 struct KArgs {
     const DevTables *T;

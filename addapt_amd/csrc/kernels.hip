@@ -1207,6 +1207,9 @@ __device__ double score_sequence(const KArgs &ka, const DevScaled *__restrict__ 
             if constexpr (P == 1 && SR::NV == 2)
                 inc.cc_dst = reinterpret_cast<uint8_t *>(base + size_t(1 - cur) * ka.tab_slot +
                                                          inc_cc_offset(ka.cells, ka.Nmax, ka.n_groups2, g));
+            if constexpr (P == 2 && SR::NV == 1 && !SR::MFE)   // PF groups (pf_cells.hip restores the codes)
+                inc.cc_dst = reinterpret_cast<uint8_t *>(base + size_t(1 - cur) * ka.tab_slot +
+                                                         inc_cc_offset_pf(ka.cells, ka.Nmax, ka.n_groups2, g));
             if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
                 const int lb = ka.variants[vs[0]].before_len;
                 inc.src = base + size_t(cur) * ka.tab_slot + size_t(g) * G;

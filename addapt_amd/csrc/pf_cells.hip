@@ -504,13 +504,18 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const size_t Cs = size_t(ka.cells), B1 = 3 * Cs + size_t(ka.Nmax) + 2;
     const float *src = nullptr;
     float *dst = nullptr;
+    const uint4 *cc_src = nullptr;   // the slots' per-cell codes (dev_types.hpp inc_cc_offset_pf)
+    uint4 *cc_dst = nullptr;
     int m_lo = 0, m_hi = 0;
     if (ka.tab) {
         const int cur = ka.cur_slot[w];
         float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
         dst = base + size_t(1 - cur) * ka.tab_slot + size_t(grp) * 2 * B1;
+        const size_t cco = inc_cc_offset_pf(ka.cells, ka.Nmax, ka.n_groups2, grp);
+        cc_dst = reinterpret_cast<uint4 *>(base + size_t(1 - cur) * ka.tab_slot + cco);
         if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
             src = base + size_t(cur) * ka.tab_slot + size_t(grp) * 2 * B1;
+            cc_src = reinterpret_cast<const uint4 *>(base + size_t(cur) * ka.tab_slot + cco);
             m_lo = ka.chg[2 * w] + 1 + V.before_len;
             m_hi = ka.chg[2 * w + 1] + 1 + V.before_len;
         }
@@ -533,6 +538,9 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     static_assert(3 * (((PX_NMAX - 4) * (PX_NMAX - 3) / 2) / 2) <= RS * PX_NT, "restore loads fit RS per lane");
     const int half = C >> 1;
     float2 rsx[RS], rsy[RS];
+    const int C16 = (C + 15) >> 4;
+    static_assert(((PX_NMAX - 4) * (PX_NMAX - 3) / 2 + 15) / 16 <= PX_NT, "one code load per thread");
+    uint4 rcv = make_uint4(0, 0, 0, 0);
     if (incr) {
 #pragma unroll
         for (int t = 0; t < RS; t++) {
@@ -543,6 +551,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             rsx[t] = *reinterpret_cast<const float2 *>(sa);
             rsy[t] = *reinterpret_cast<const float2 *>(sa + B1);
         }
+        rcv = cc_src[tid < C16 ? tid : 0];   // the codes (round 6: the band's are recomputed)
     } else {
         for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
     }
@@ -642,6 +651,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             for (int a = tid; a < 3; a += PX_NT) {
                 L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
             }
+        if (tid < C16) reinterpret_cast<uint4 *>(L.cc)[tid] = rcv;
         for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
     }
     __syncthreads();
@@ -661,9 +671,10 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     for (int D = 4 + wid; D <= N - 1; D += PX_NW) {
         const int od = off(D, N), lo = clo(D), hi = chi(D);
         int base = 0;
-        for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
+        // a refold's band rows only (round 6: the other cells' codes are restored)
+        for (int i0 = lo; i0 <= hi; i0 += WAVE) {
             const int i = i0 + lane;
-            const bool cell = i <= N - D;
+            const bool cell = i <= hi;
             const bool inb = cell && i >= lo && i <= hi;
             bool pr = false;
             if (cell) {
@@ -1041,6 +1052,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             dst[3 * Cs + k] = L.q5[k].x;
             dst[B1 + 3 * Cs + k] = L.q5[k].y;
         }
+        for (int k = tid; k < ((C + 15) >> 4); k += PX_NT) cc_dst[k] = reinterpret_cast<const uint4 *>(L.cc)[k];
     }
     if (tid == 0) {   // ensemble energy -kT (ln Z_scaled - N ln sigma), as vrna_pf (float)
         const f2 z = L.q5[N];
