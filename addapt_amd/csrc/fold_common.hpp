@@ -65,6 +65,31 @@ __device__ __forceinline__ bool mfe16_inexact(s16x2 q) {
     return out(q.x) || out(q.y);
 }
 
+// Index of the special hairpin whose key is `key` in spk[0, MAX_SPECIAL_HP) (LDS,
+// 16-byte aligned, padded with 0xFFFFFFFF, which hp_key never returns), or -1; the
+// last match, as a scan would find.  Every key comes in wave-uniform 16-byte loads
+// issued before any compare: the compare -> value-load chain per key it replaces
+// serialised ~16 LDS round trips per 8 keys, ~10k cycles per cell-pass item on the
+// special-hairpin diagonals (stamps, profiles/r06s_mfe_pair_stamps_setup.txt)
+__device__ __forceinline__ int special_hp(const uint32_t *spk, uint32_t key) {
+    static_assert(MAX_SPECIAL_HP % 16 == 0, "whole 16-key chunks");
+    int hit = -1;
+#pragma unroll
+    for (int q0 = 0; q0 < MAX_SPECIAL_HP; q0 += 16) {
+        uint4 k[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) k[t] = reinterpret_cast<const uint4 *>(spk + q0)[t];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            hit = k[t].x == key ? q0 + 4 * t : hit;
+            hit = k[t].y == key ? q0 + 4 * t + 1 : hit;
+            hit = k[t].z == key ? q0 + 4 * t + 2 : hit;
+            hit = k[t].w == key ? q0 + 4 * t + 3 : hit;
+        }
+    }
+    return hit;
+}
+
 // Pair type / reversed type / terminal-AU flag without a memory lookup:
 // PAIR[a][b] for codes a, b in 0..4 (ViennaRNA types 1..6) packed 3 bits per
 // entry of index 5a+b-9 (the canonical pairs sit at 9..23).

@@ -192,6 +192,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
 #ifdef ADX_STAMP
     const unsigned long long st_setup0 = __builtin_amdgcn_s_memtime();
 #endif
+    // hairpin length factors of this wave's per-cell-pass diagonals d = 4 + wid + 8m
+    // (lane m; read back by readlane), loaded first so no pass waits on HBM
+    const u32 hpl = __float_as_uint(XS->hp[min(3 + wid + NWV * lane, NMAX)]);
     const bool incr = inc.src != nullptr;
     const int m_lo = uni(inc.m_lo), m_hi = uni(inc.m_hi);
     // changed rows of span dd (cells containing a changed position; mfe_cells.hip)
@@ -200,10 +203,98 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     auto qlo = [&](int s) { return incr ? max(1, m_lo - 2 - s) : 1; };
     auto qhi = [&](int s) { return incr ? min(N - s, m_hi + 2) : N - s; };
 
-    // ---- refold restore: the loads of all three tables are issued first (8-byte
-    // vector loads into registers) and stored to LDS after the motif scan, so
-    // their HBM latency overlaps the sequence / motif setup (round 6; the loop of
-    // dependent load -> store pairs cost ~20k cycles per fold group)
+    // ---- setup loads (round 6): every table element and sequence / constraint byte this
+    // thread stores, all in flight at once and stored before the restore's loads are
+    // issued (the kernel prologue's loop per table waited on each load in turn, and the
+    // setup tables' loads waited behind the restore's)
+    static_assert(NT >= 288 && NT >= MAX_SPECIAL_HP && NT >= MAX_MOTIF && NT >= MFE_E4_SLOTS * 4 && NT >= NM + 2,
+                  "one setup element per thread");
+    constexpr int NCT = (CT_SIZE + NT - 1) / NT;
+    u32 v_ct[NCT];
+#pragma unroll
+    for (int t = 0; t < NCT; t++) v_ct[t] = gct[min(tid + t * NT, CT_SIZE - 1)];
+    const DevTables &T0 = *TT;
+    const u32 v_mh = __float_as_uint((&T0.mmH[0][0][0])[min(tid, 199)]);
+    const u32 v_mi = __float_as_uint((&T0.mmI[0][0][0])[min(tid, 199)]);
+    const u32 v_ms = __float_as_uint((&T0.mlstem[0][0][0])[min(tid, 199)]);
+    const u32 v_ex = __float_as_uint((&T0.ext[0][0][0])[min(tid, 287)]);
+    const u32 v_tau = __float_as_uint(T0.termAU[tid & 7]);
+    const int ke = min(tid, MFE_E4_SLOTS * 4 - 1);
+    const int e4a = MFE_E4_A[ke >> 2][ke & 3], e4u = MFE_E4_U[ke >> 2];
+    const int n_sp = XS->n_special;
+    const uint32_t v_spk = XS->sp_key[min(tid, MAX_SPECIAL_HP - 1)];
+    const u32 v_spv = __float_as_uint(XS->sp_val[min(tid, MAX_SPECIAL_HP - 1)]);
+    const uint8_t v_mc = XS->motif_code[min(tid, MAX_MOTIF - 1)];
+    const int8_t v_mp = XS->motif_pt[min(tid, MAX_MOTIF - 1)];
+    // position k = tid: its base (ViennaRNA's S1 wrap-around at 0 and N + 1) and constraints
+    const uint8_t *cons = ka.cons + V.cons_off;
+    const int np = N + 2;
+    const int kp = min(tid, np - 1);
+    uint8_t v_sw, v_up, v_dn, v_pt, v_en, v_fl;
+    {
+        const uint8_t *bef = nullptr, *aft = nullptr;
+        int blen = 0;
+        if (V.ctx >= 0) {
+            bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
+            blen = ka.ctx_off[4 * V.ctx + 1];
+            aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
+        }
+        const int pp = (kp == 0 ? N : (kp == N + 1 ? 1 : kp)) - 1;
+        const uint8_t *sp = pp < blen ? bef + pp : (pp < blen + ka.Nraw ? raw + (pp - blen) : aft + (pp - blen - ka.Nraw));
+        v_sw = *sp;
+        v_up = cons[kp];
+        v_dn = cons[np + kp];
+        v_pt = cons[2 * np + kp];
+        v_en = cons[3 * np + kp];
+        v_fl = cons[4 * np + kp];
+    }
+    // ---- the stores: sequence, constraint arrays (mfe_cells.hip), tables
+    if (tid < np) {
+        L.S[tid] = v_sw;
+        L.up[tid] = v_up;
+        L.dn[tid] = v_dn;
+        L.ptn[tid] = v_pt;
+        L.enc[tid] = v_en;
+        L.flg[tid] = v_fl;
+        L.mat[tid] = 0;
+        L.pos[tid] = u32(v_sw) | (u32(v_fl & 7) << 3) | (u32(v_up) << 8) | (u32(v_pt) << 16) | (u32(v_en) << 24);
+    }
+    const bool cst = tid >= 1 && tid <= N && (v_fl || v_pt);
+#pragma unroll
+    for (int t = 0; t < NCT; t++)
+        if (tid + t * NT < CT_SIZE) L.ct[tid + t * NT] = v_ct[t];
+    if (tid < 200) {
+        L.dt[DT_MMH + tid] = v_mh;
+        L.dt[DT_MMI + tid] = v_mi;
+        L.dt[DT_MLS + tid] = v_ms;
+    }
+    if (tid < 288) L.dt[DT_EXT + tid] = v_ex;
+    if (tid < 8) L.dt[DT_TAU + tid] = v_tau;
+    // setup scratch in the partial / split / U slots (first written after the per-cell pass)
+    uint32_t *spk = reinterpret_cast<uint32_t *>(L.part);
+    u32 *spv = spk + MAX_SPECIAL_HP;
+    uint8_t *mcode = reinterpret_cast<uint8_t *>(spk + 2 * MAX_SPECIAL_HP);
+    int8_t *mpt = reinterpret_cast<int8_t *>(mcode + MAX_MOTIF);
+    static_assert(2 * MAX_SPECIAL_HP * 4 + 2 * MAX_MOTIF <= PLay<NM>::MLA - PLay<NM>::PART, "setup tables fit the partials");
+    if (tid < MAX_SPECIAL_HP) {
+        const bool on = tid < n_sp;
+        spk[tid] = on ? v_spk : 0xFFFFFFFFu;
+        spv[tid] = on ? v_spv : INF16;
+    }
+    if (tid < MAX_MOTIF) {
+        mcode[tid] = v_mc;
+        mpt[tid] = v_mp;
+    }
+    for (int k = tid; k < NM - 3; k += NT) {   // the impossible span-3 diagonal (B's d-lanes reach it)
+        (L.qbm - (NM - 3))[k] = INF16;
+        (L.cc - (NM - 3))[k] = 0;
+    }
+
+    // ---- refold restore: the loads of all three tables (8-byte vector loads into
+    // registers), stored to LDS after the motif scan, so their HBM latency overlaps
+    // it (round 6; the loop of dependent load -> store pairs cost ~20k cycles per
+    // fold group).  The generic interior energies of the 4-lane blocks (e4) ride along.
+    const u32 v_e4 = XS->ku16[e4u][max(e4a, 0)];
     constexpr int CNM = ((NM - 4) * (NM - 3)) >> 1;
     constexpr int RS = (3 * (CNM >> 1) + NT - 1) / NT;   // loads per thread
     const int Crs = ((N - 4) * (N - 3)) >> 1, half = Crs >> 1;
@@ -211,6 +302,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     constexpr int RC = (((CNM + 15) >> 4) + NT - 1) / NT;   // per-cell code loads per thread (uint4)
     const int C16 = (Crs + 15) >> 4;
     uint4 rcv[RC];
+    u32 rod = 0, r5 = 0;   // the odd last cell of each table, q5's prefix
     if (incr) {
         const size_t Cs = size_t(ka.cells);
 #pragma unroll
@@ -225,69 +317,16 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             const int k = tid + t * NT;
             rcv[t] = inc.cc_src[k < C16 ? k : 0];
         }
-    }
-    // setup scratch in the partial / split / U slots (first written after the per-cell pass)
-    uint32_t *spk = reinterpret_cast<uint32_t *>(L.part);
-    u32 *spv = spk + MAX_SPECIAL_HP;
-    uint8_t *mcode = reinterpret_cast<uint8_t *>(spk + 2 * MAX_SPECIAL_HP);
-    int8_t *mpt = reinterpret_cast<int8_t *>(mcode + MAX_MOTIF);
-    static_assert(2 * MAX_SPECIAL_HP * 4 + 2 * MAX_MOTIF <= PLay<NM>::MLA - PLay<NM>::PART, "setup tables fit the partials");
-    for (int k = tid; k < MAX_SPECIAL_HP; k += NT) {
-        const bool on = k < XS->n_special;
-        spk[k] = on ? XS->sp_key[k] : 0xFFFFFFFFu;
-        spv[k] = on ? __float_as_uint(XS->sp_val[k]) : INF16;
-    }
-    for (int k = tid; k < MAX_MOTIF; k += NT) {
-        mcode[k] = XS->motif_code[k];
-        mpt[k] = XS->motif_pt[k];
-    }
-    for (int k = tid; k < NM - 3; k += NT) {   // the impossible span-3 diagonal (B's d-lanes reach it)
-        (L.qbm - (NM - 3))[k] = INF16;
-        (L.cc - (NM - 3))[k] = 0;
-    }
-
-#ifdef ADX_STAMP
-    const unsigned long long st_s1 = __builtin_amdgcn_s_memtime();   // restore issued, setup tables
-#endif
-    // ---- sequence, constraint arrays, motif sites (mfe_cells.hip)
-    const uint8_t *cons = ka.cons + V.cons_off;
-    const int np = N + 2;
-    const uint8_t *bef = nullptr, *aft = nullptr;
-    int blen = 0;
-    if (V.ctx >= 0) {
-        bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
-        blen = ka.ctx_off[4 * V.ctx + 1];
-        aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
-    }
-    bool constrained = false;
-    auto seq_at = [&](int k) -> uint8_t {   // base of position k (1..N)
-        const int pp = k - 1;
-        return pp < blen ? bef[pp] : (pp < blen + ka.Nraw ? raw[pp - blen] : aft[pp - blen - ka.Nraw]);
-    };
-    for (int k = tid; k < np; k += NT) {
-        const uint8_t s = (k >= 1 && k <= N) ? seq_at(k) : 0;
-        L.S[k] = s;
-        const uint8_t f = cons[4 * np + k], pt = cons[2 * np + k], up = cons[k], en = cons[3 * np + k];
-        L.up[k] = up;
-        L.dn[k] = cons[np + k];
-        L.ptn[k] = pt;
-        L.enc[k] = en;
-        L.flg[k] = f;
-        L.mat[k] = 0;
-        // ViennaRNA's S1 wrap-around in the words (L.S gets it below)
-        const uint8_t sw = k == 0 ? seq_at(N) : (k == N + 1 ? seq_at(1) : s);
-        L.pos[k] = u32(sw) | (u32(f & 7) << 3) | (u32(up) << 8) | (u32(pt) << 16) | (u32(en) << 24);
-        if (k >= 1 && k <= N && (f || pt)) constrained = true;
-    }
-    if (!incr) {
+        rod = inc.src[min(tid, 2) * Cs + max(Crs - 1, 0)];
+        r5 = inc.src[3 * Cs + min(tid, N)];
+    } else {
         const int C = ((N - 4) * (N - 3)) >> 1;
         for (int k = tid; k < C; k += NT) L.qm[k] = INF16;
     }
-    constrained = block_or(L.flag, constrained);
-    if (tid == 0) {
-        L.S[0] = L.S[N];
-        L.S[N + 1] = L.S[1];
-    }
+#ifdef ADX_STAMP
+    const unsigned long long st_s1 = __builtin_amdgcn_s_memtime();   // setup tables stored, restore issued
+#endif
+    const bool constrained = block_or(L.flag, cst);
     const int mL = XS->motif_len;
 #ifdef ADX_STAMP
     const unsigned long long st_s2 = __builtin_amdgcn_s_memtime();   // sequence, constraints
@@ -325,6 +364,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             if (lane == 0) L.mat[o] = all ? 1 : 0;
         }
     }
+#ifdef ADX_STAMP
+    const unsigned long long st_s25 = __builtin_amdgcn_s_memtime();   // motif scan done
+#endif
     if (incr) {   // the restore's stores (loads issued at the start)
         const size_t Cs = size_t(ka.cells);
 #pragma unroll
@@ -336,15 +378,15 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                 *reinterpret_cast<uint2 *>(d + 2 * c) = rsv[t];
             }
         }
-        if (Crs & 1)
-            for (int a = tid; a < 3; a += NT) (a == 0 ? L.qbm : a == 1 ? L.qm : L.qm1)[Crs - 1] = inc.src[a * Cs + Crs - 1];
+        if ((Crs & 1) && tid < 3) (tid == 0 ? L.qbm : tid == 1 ? L.qm : L.qm1)[Crs - 1] = rod;
 #pragma unroll
         for (int t = 0; t < RC; t++) {   // the codes (16 cells per store; the band's are recomputed)
             const int k = tid + t * NT;
             if (k < C16) reinterpret_cast<uint4 *>(L.cc)[k] = rcv[t];
         }
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += NT) L.q5[k] = inc.src[3 * Cs + k];
+        if (tid <= m_lo - 2 && tid <= N) L.q5[tid] = r5;
     }
+    if (tid < MFE_E4_SLOTS * 4) L.e4[tid] = e4a < 0 ? INF16 : v_e4;
     __syncthreads();
     const u32 mlclosing = __float_as_uint(XS->mlclosing);
     const u32 mlbase = __float_as_uint(XS->mlbase_sig);
@@ -414,14 +456,10 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             L.cc[off(d, N) + i - 1] = static_cast<uint8_t>(rtype(ty[q]) * 25 + (wjp[q] & 7) * 5 + (wim[q] & 7));
             u32 h = INF16;
             if (((wi1[q] >> 8) & 255) >= uint32_t(u)) {
-                h = padd(__float_as_uint(XS->hp[u]), f1[q]);
+                h = padd(u32(__builtin_amdgcn_readlane(int(hpl), (d - 4 - wid) / NWV)), f1[q]);
                 if (u == 3 || u == 4 || u == 6) {   // special hairpins (three diagonals)
-                    const uint32_t key = hp_key(L.S, i, u + 2);
-                    for (int q0 = 0; q0 < nsp; q0 += 8) {
-#pragma unroll
-                        for (int t = 0; t < 8; t++)
-                            if (spk[q0 + t] == key) h = spv[q0 + t];
-                    }
+                    const int sh = special_hp(spk, hp_key(L.S, i, u + 2));
+                    if (sh >= 0) h = spv[sh];
                 }
             }
             if (d == mL - 1 && mL > 0 && mt[q]) h = pmin(h, mextra);
@@ -431,7 +469,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             }
         }
     };
+    static_assert(4 + (WAVE - 1) * NWV > NMAX, "hpl covers every diagonal");
     for (int dd = 4 + wid; dd <= N - 1; dd += 2 * NWV) cell_pass(dd);
+#ifdef ADX_STAMP
+    const unsigned long long st_s35 = __builtin_amdgcn_s_memtime();   // this wave's cells (before the barrier)
+#endif
     __syncthreads();
 #ifdef ADX_STAMP
     const unsigned long long st_s4 = __builtin_amdgcn_s_memtime();   // per-cell pass
@@ -525,12 +567,14 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     auto hi2 = [](u32 x) { return __builtin_amdgcn_perm(x, x, 0x07060706u); };
 
 #ifdef ADX_STAMP
-    unsigned long long st_acc[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
     st_acc[8] = st_last - st_setup0;
     st_acc[11] = st_s1 - st_setup0;
     st_acc[12] = st_s2 - st_s1;
-    st_acc[13] = st_s3 - st_s2;
+    st_acc[13] = st_s25 - st_s2;
+    st_acc[7] = st_s3 - st_s25;
+    st_acc[15] = st_s35 - st_s3;
     st_acc[14] = st_s4 - st_s3;
 #endif
     int sl = 0;   // list slot of this step: step index % 3
@@ -1022,7 +1066,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     }
 #ifdef ADX_STAMP
     if (lane == 0 && wid < 16)
-        for (int k = 0; k < 15; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
+        for (int k = 0; k < 16; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
 #endif
     z = L.q5[N];
     if (inc.dst) {   // this fold's tables: the next proposal's unchanged cells
@@ -1056,8 +1100,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
 template <int NT, int NM, int... Ws>
 __device__ __forceinline__ void pair_fold_wave(std::integer_sequence<int, Ws...>, int w, const KArgs &ka,
                                                const DevScaled *__restrict__ XS, const DevTables *__restrict__ TT,
-                                               const int *vs, const CP &L, u32 &z, bool &bad, const IncM &inc) {
-    ((w == Ws ? (mfe_pair_fold<NT, NM, Ws>(ka, XS, TT, vs, L.raw, L, z, bad, inc), 0) : 0), ...);
+                                               const int *vs, const uint8_t *seqs, const CP &L, u32 &z, bool &bad,
+                                               const IncM &inc) {
+    ((w == Ws ? (mfe_pair_fold<NT, NM, Ws>(ka, XS, TT, vs, seqs, L, z, bad, inc), 0) : 0), ...);
 }
 
 constexpr int MFE_WPE = (2 * NWV + 3) / 4;
@@ -1072,25 +1117,7 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     if (wb >= W) return;
     const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
     if (w < 0) return;
-    {
-        const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
-        for (int k = threadIdx.x; k < CT_SIZE; k += NT) L.ct[k] = gct[k];
-        const DevTables &T = *TT;
-        auto bits = [](float f) { return __float_as_uint(f); };
-        for (int k = threadIdx.x; k < 200; k += NT) {
-            L.dt[DT_MMH + k] = bits((&T.mmH[0][0][0])[k]);
-            L.dt[DT_MMI + k] = bits((&T.mmI[0][0][0])[k]);
-            L.dt[DT_MLS + k] = bits((&T.mlstem[0][0][0])[k]);
-        }
-        for (int k = threadIdx.x; k < 288; k += NT) L.dt[DT_EXT + k] = bits((&T.ext[0][0][0])[k]);
-        for (int k = threadIdx.x; k < 8; k += NT) L.dt[DT_TAU + k] = bits(T.termAU[k]);
-        for (int k = threadIdx.x; k < ka.Nraw; k += NT) L.raw[k] = seqs[size_t(w) * ka.Nraw + k];
-        if (threadIdx.x < 2) L.flag[threadIdx.x] = 0;
-        for (int k = threadIdx.x; k < MFE_E4_SLOTS * 4; k += NT) {
-            const int a = MFE_E4_A[k >> 2][k & 3];
-            L.e4[k] = a < 0 ? INF16 : XS->ku16[MFE_E4_U[k >> 2]][a];
-        }
-    }
+    if (threadIdx.x < 2) L.flag[threadIdx.x] = 0;
     __syncthreads();
     const int vs[2] = {ka.groups2[2 * g], ka.groups2[2 * g + 1]};
     IncM inc{nullptr, nullptr, 0, 0, nullptr, nullptr};
@@ -1113,8 +1140,8 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     }
     u32 z = INF16;
     bool bad = false;
-    pair_fold_wave<NT, NM>(std::make_integer_sequence<int, NWV>{}, uni(int(threadIdx.x) / WAVE), ka, XS, TT, vs, L, z,
-                           bad, inc);
+    pair_fold_wave<NT, NM>(std::make_integer_sequence<int, NWV>{}, uni(int(threadIdx.x) / WAVE), ka, XS, TT, vs,
+                           seqs + size_t(w) * ka.Nraw, L, z, bad, inc);
     if (threadIdx.x == 0) {
         const s16x2 q = sv(z);
         const int hv[2] = {q.x, q.y};

@@ -529,6 +529,76 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
     auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
 
+    // ---- setup loads (round 6): the one element of every table and of the sequence /
+    // constraint arrays this thread stores, all in flight at once and stored before
+    // the restore's loads are issued (a loop per table waited on each load in turn, the
+    // first behind the restore's: ~14k cycles per group, stamps r06p "tables")
+    static_assert(CT_SIZE <= PX_NT && 288 <= PX_NT && PX_NMAX + 9 <= PX_NT && MAX_SPECIAL_HP <= PX_NT &&
+                  MAX_MOTIF <= PX_NT && PX_NMAX + 2 <= PX_NT, "one setup element per thread");
+    const float v_ct = XS->ctab[min(tid, CT_SIZE - 1)];
+    const float v_mh = (&T.mmH[0][0][0])[min(tid, 199)], v_mi = (&T.mmI[0][0][0])[min(tid, 199)],
+                v_ms = (&T.mlstem[0][0][0])[min(tid, 199)];
+    const float v_ex = (&T.ext[0][0][0])[min(tid, 287)], v_tau = T.termAU[tid & 7];
+    const float v_pw = XS->pwml[min(tid, N + 8)];
+    const int n_sp = XS->n_special;
+    const uint32_t v_spk = XS->sp_key[min(tid, MAX_SPECIAL_HP - 1)];
+    const float v_spv = XS->sp_val[min(tid, MAX_SPECIAL_HP - 1)];
+    const uint8_t v_mc = XS->motif_code[min(tid, MAX_MOTIF - 1)];
+    const int8_t v_mp = XS->motif_pt[min(tid, MAX_MOTIF - 1)];
+    // hairpin length factors of this wave's per-cell-pass diagonals D = 4 + wid + NW m (lane m)
+    static_assert(4 + (WAVE - 1) * PX_NW > PX_NMAX, "hpl covers every diagonal");
+    const float hpl = XS->hp[min(3 + wid + PX_NW * lane, NMAX)];
+    const uint8_t *cons = ka.cons + V.cons_off;
+    const int kp = min(tid, NP - 1);   // this thread's position
+    uint8_t v_s, v_up, v_dn, v_pt, v_en, v_fl;
+    {
+        const uint8_t *bef = nullptr, *aft = nullptr;
+        int blen = 0;
+        if (V.ctx >= 0) {
+            bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
+            blen = ka.ctx_off[4 * V.ctx + 1];
+            aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
+        }
+        const uint8_t *raw = seqs + size_t(w) * ka.Nraw;
+        const int pp = kp >= 1 && kp <= N ? kp - 1 : blen;   // outside 1..N: a valid byte, discarded
+        const uint8_t *sp = pp < blen ? bef + pp : (pp < blen + ka.Nraw ? raw + (pp - blen) : aft + (pp - blen - ka.Nraw));
+        v_s = *sp;
+        v_up = cons[kp];
+        v_dn = cons[NP + kp];
+        v_pt = cons[2 * NP + kp];
+        v_en = cons[3 * NP + kp];
+        v_fl = cons[4 * NP + kp];
+    }
+
+    // ---- sequence, constraint arrays, tables (kernels.hip pf_group setup): the stores
+    if (tid < NP) {
+        L.S[tid] = (tid >= 1 && tid <= N) ? v_s : 0;
+        L.up[tid] = v_up;
+        L.dn[tid] = v_dn;
+        L.ptn[tid] = v_pt;
+        L.enc[tid] = v_en;
+        L.flg[tid] = v_fl;
+        L.mat[tid] = 0;
+    }
+    const bool cst = tid >= 1 && tid <= N && (v_fl | v_pt) != 0;
+    if (tid < CT_SIZE) L.ct[tid] = v_ct;
+    if (tid < 200) {
+        L.dt[DT_MMH + tid] = v_mh;
+        L.dt[DT_MMI + tid] = v_mi;
+        L.dt[DT_MLS + tid] = v_ms;
+    }
+    if (tid < 288) L.dt[DT_EXT + tid] = v_ex;
+    if (tid < 8) L.dt[DT_TAU + tid] = v_tau;
+    if (tid < N + 9) L.pw[tid] = v_pw;
+    if (tid < MAX_SPECIAL_HP) {
+        const bool on = tid < n_sp;
+        spk[tid] = on ? v_spk : 0xFFFFFFFFu;   // hp_key never sets the top bits
+        spv[tid] = on ? v_spv : 0.f;
+    }
+    if (tid < MAX_MOTIF) {
+        mcode[tid] = v_mc;
+        mpt[tid] = v_mp;
+    }
     // ---- refold restore: every table from the current slot (the changed cells are
     // recomputed over it), two cells per lane and load, both folds interleaved.
     // The loads are issued here and stored to LDS after the motif scan, so their
@@ -541,6 +611,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const int C16 = (C + 15) >> 4;
     static_assert(((PX_NMAX - 4) * (PX_NMAX - 3) / 2 + 15) / 16 <= PX_NT, "one code load per thread");
     uint4 rcv = make_uint4(0, 0, 0, 0);
+    f2 rod = f2{0.f, 0.f}, r5 = f2{0.f, 0.f};
     if (incr) {
 #pragma unroll
         for (int t = 0; t < RS; t++) {
@@ -552,56 +623,12 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             rsy[t] = *reinterpret_cast<const float2 *>(sa + B1);
         }
         rcv = cc_src[tid < C16 ? tid : 0];   // the codes (round 6: the band's are recomputed)
+        const int ko = min(tid, 2);           // the odd last cell of each table, q5's prefix
+        rod = f2{src[ko * Cs + max(C - 1, 0)], src[B1 + ko * Cs + max(C - 1, 0)]};
+        const int k5 = min(tid, N);
+        r5 = f2{src[3 * Cs + k5], src[B1 + 3 * Cs + k5]};
     } else {
         for (int k = tid; k < C; k += PX_NT) L.qm[k] = f2{0.f, 0.f};   // spans N-2, N-1 are never computed
-    }
-    // ---- sequence, constraint arrays, tables (kernels.hip pf_group setup)
-    const uint8_t *cons = ka.cons + V.cons_off;
-    {
-        const uint8_t *bef = nullptr, *aft = nullptr;
-        int blen = 0;
-        if (V.ctx >= 0) {
-            bef = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 0];
-            blen = ka.ctx_off[4 * V.ctx + 1];
-            aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
-        }
-        const uint8_t *raw = seqs + size_t(w) * ka.Nraw;
-        for (int k = tid; k < NP; k += PX_NT) {
-            uint8_t s = 0;
-            if (k >= 1 && k <= N) {
-                const int pp = k - 1;
-                if (pp < blen) s = bef[pp];
-                else if (pp < blen + ka.Nraw) s = raw[pp - blen];
-                else s = aft[pp - blen - ka.Nraw];
-            }
-            L.S[k] = s;
-            L.up[k] = cons[k];
-            L.dn[k] = cons[NP + k];
-            L.ptn[k] = cons[2 * NP + k];
-            L.enc[k] = cons[3 * NP + k];
-            L.flg[k] = cons[4 * NP + k];
-            L.mat[k] = 0;
-        }
-    }
-    bool cst = false;
-    for (int k = 1 + tid; k <= N; k += PX_NT) cst |= (L.flg[k] | L.ptn[k]) != 0;
-    for (int k = tid; k < CT_SIZE; k += PX_NT) L.ct[k] = XS->ctab[k];
-    for (int k = tid; k < 200; k += PX_NT) {
-        L.dt[DT_MMH + k] = (&T.mmH[0][0][0])[k];
-        L.dt[DT_MMI + k] = (&T.mmI[0][0][0])[k];
-        L.dt[DT_MLS + k] = (&T.mlstem[0][0][0])[k];
-    }
-    for (int k = tid; k < 288; k += PX_NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
-    for (int k = tid; k < 8; k += PX_NT) L.dt[DT_TAU + k] = T.termAU[k];
-    for (int k = tid; k < N + 9; k += PX_NT) L.pw[k] = XS->pwml[k];
-    for (int k = tid; k < MAX_SPECIAL_HP; k += PX_NT) {
-        const bool on = k < XS->n_special;
-        spk[k] = on ? XS->sp_key[k] : 0xFFFFFFFFu;   // hp_key never sets the top bits
-        spv[k] = on ? XS->sp_val[k] : 0.f;
-    }
-    for (int k = tid; k < MAX_MOTIF; k += PX_NT) {
-        mcode[k] = XS->motif_code[k];
-        mpt[k] = XS->motif_pt[k];
     }
     for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
     for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
@@ -647,12 +674,10 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                 qd[a * ls4 + c] = float4{rsx[t].x, rsy[t].x, rsx[t].y, rsy[t].y};
             }
         }
-        if (C & 1)
-            for (int a = tid; a < 3; a += PX_NT) {
-                L.qb[a * (ls4 * 2) + C - 1] = f2{src[a * Cs + C - 1], src[B1 + a * Cs + C - 1]};
-            }
+        if ((C & 1) && tid < 3) L.qb[tid * (ls4 * 2) + C - 1] = rod;
         if (tid < C16) reinterpret_cast<uint4 *>(L.cc)[tid] = rcv;
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += PX_NT) L.q5[k] = f2{src[3 * Cs + k], src[B1 + 3 * Cs + k]};
+        static_assert(PX_NMAX < PX_NT, "one q5 entry per thread");
+        if (tid <= m_lo - 2 && tid <= N) L.q5[tid] = r5;
     }
     __syncthreads();
     PSTAMP(7);   // motif sites + the restore's stores (the wait for its loads)
@@ -691,15 +716,14 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
                         if (L.up[i + 1] >= u) {
                             bool special = false;
                             if (u == 3 || u == 4 || u == 6) {
-                                const uint32_t key = hp_key(S, i, u + 2);
-                                for (int q0 = 0; q0 < nsp; q0 += 8) {   // 8 independent LDS reads per round
-#pragma unroll
-                                    for (int t = 0; t < 8; t++)
-                                        if (spk[q0 + t] == key) { h = spv[q0 + t]; special = true; }
+                                const int sh = special_hp(spk, hp_key(S, i, u + 2));
+                                if (sh >= 0) {
+                                    h = spv[sh];
+                                    special = true;
                                 }
                             }
                             if (!special)
-                                h = XS->hp[u] * ((u == 3) ? L.dt[DT_TAU + type]
+                                h = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hpl), (D - 4 - wid) / PX_NW)) * ((u == 3) ? L.dt[DT_TAU + type]
                                                                 : L.dt[DT_MMH + type * 25 + S[i + 1] * 5 + S[j - 1]]);
                         }
                         const bool mx = D == mL - 1 && mL > 0 && L.mat[i];

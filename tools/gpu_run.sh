@@ -10,6 +10,7 @@
 #   prof:<name>:<bench.py args>     rocprofv3 --kernel-trace --stats of a bench run
 #   pmc:<name>:<bench.py args>      three PMC passes (SQ occupancy / instruction
 #                                   mix / LDS), kernel trace only, per dispatch
+#   pmcx:<name>:<counters,...>:<bench.py args>   one PMC pass of the listed counters
 #   traffic:<name>:<kernel>:<bench.py args>   FETCH_SIZE + WRITE_SIZE passes ->
 #                                   traffic_latest_<name>.json (tools/pmc_traffic.py)
 #   py:<name>:<script args>         a tools/ script (e.g. 'py:stamp_mfe:tools/pf_stamps.py 100 mfe';
@@ -53,6 +54,12 @@ for step in "$@"; do
         timeout -k 10 120 rocprofv3 --pmc $grp -d $D/pmc_$name/p$i -o g$i --output-format csv \
           -- python bench.py $args --steps 2 --warmup 1 --no-cpu-baseline --no-sub-records > $D/pmc_${name}_$i.txt 2>&1
       done ;;
+    pmcx)   # one PMC pass of the given counters: pmcx:<name>:<counters, comma-separated>:<bench.py args>
+      ctrs=${args%%:*}
+      bargs=${args#*:}
+      [ "$ctrs" = "$args" ] && bargs=
+      timeout -k 10 120 rocprofv3 --pmc ${ctrs//,/ } -d $D/pmcx_$name -o x --output-format csv \
+        -- python bench.py $bargs --steps 2 --warmup 1 --no-cpu-baseline --no-sub-records > $D/pmcx_$name.txt 2>&1 ;;
     traffic)
       kern=${args%%:*}
       bargs=${args#*:}

@@ -30,12 +30,12 @@ _, _, c = eng.download()
 scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = scored * 2   # fold groups
 cols = ["setup", "top", "L", "F", "Bcell", "Bblock", "Bfold", "M", "Q", "barrier", "total",
-        "s.restore", "s.seq", "s.motif", "s.cells"]
+        "s.restore", "s.seq", "s.motif", "s.rstore", "s.cells", "s.cellw"]
 print("cycles per fold group per wave (N=%d, W=%d, %d steps, %.0f groups)" % (N, W, steps, G))
 print("wave " + " ".join("%8s" % n for n in cols))
 for w in range(16):
     if not any(buf[w * 16 + k] for k in range(16)):
         continue
     v = [buf[w * 16 + k] // max(1, G) for k in (8, 0, 1, 2, 9, 10, 3, 4, 5, 6)]
-    sub = [buf[w * 16 + k] // max(1, G) for k in (11, 12, 13, 14)]
+    sub = [buf[w * 16 + k] // max(1, G) for k in (11, 12, 13, 7, 14, 15)]  # s.cellw: this wave's cell pass before the barrier
     print("%4d " % w + " ".join("%8d" % x for x in v) + " %8d" % sum(v) + " " + " ".join("%8d" % x for x in sub))
