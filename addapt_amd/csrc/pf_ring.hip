@@ -463,8 +463,27 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
     auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
 
-    // ---- sequence, constraint arrays, tables
+    // ---- sequence, constraint arrays, tables (round 6, as pf_cells.hip): the one or
+    // two elements of each this thread stores, all loads in flight at once, then the
+    // stores (a loop per table waited on each load in turn)
+    static_assert(288 <= RG_NT && RG_NMAX + 9 <= RG_NT && MAX_SPECIAL_HP <= RG_NT && MAX_MOTIF <= RG_NT,
+                  "one setup element per thread");
+    constexpr int NCT = (CT_SIZE + RG_NT - 1) / RG_NT;
+    float v_ct[NCT];
+#pragma unroll
+    for (int t = 0; t < NCT; t++) v_ct[t] = XS->ctab[min(tid + t * RG_NT, CT_SIZE - 1)];
+    const float v_mh = (&T.mmH[0][0][0])[min(tid, 199)], v_mi = (&T.mmI[0][0][0])[min(tid, 199)],
+                v_ms = (&T.mlstem[0][0][0])[min(tid, 199)];
+    const float v_ex = (&T.ext[0][0][0])[min(tid, 287)], v_tau = T.termAU[tid & 7];
+    const float v_hp = XS->hp[min(tid, N)], v_pw = XS->pwml[min(tid, N + 8)];
+    const int n_sp = XS->n_special;
+    const uint32_t v_spk = XS->sp_key[min(tid, MAX_SPECIAL_HP - 1)];
+    const float v_spv = XS->sp_val[min(tid, MAX_SPECIAL_HP - 1)];
+    const uint8_t v_mc = XS->motif_code[min(tid, MAX_MOTIF - 1)];
+    const int8_t v_mp = XS->motif_pt[min(tid, MAX_MOTIF - 1)];
     const uint8_t *cons = ka.cons + V.cons_off;
+    const int kp = min(tid, NP - 1);   // this thread's position
+    uint8_t v_s, v_up, v_dn, v_pt, v_en, v_fl;
     {
         const uint8_t *bef = nullptr, *aft = nullptr;
         int blen = 0;
@@ -474,43 +493,46 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
             aft = ka.ctx_seq + ka.ctx_off[4 * V.ctx + 2];
         }
         const uint8_t *raw = seqs + size_t(w) * ka.Nraw;
-        for (int k = tid; k < NP; k += RG_NT) {
-            uint8_t s = 0;
-            if (k >= 1 && k <= N) {
-                const int pp = k - 1;
-                if (pp < blen) s = bef[pp];
-                else if (pp < blen + ka.Nraw) s = raw[pp - blen];
-                else s = aft[pp - blen - ka.Nraw];
-            }
-            L.S[k] = s;
-            L.up[k] = cons[k];
-            L.dn[k] = cons[NP + k];
-            L.ptn[k] = cons[2 * NP + k];
-            L.enc[k] = cons[3 * NP + k];
-            L.flg[k] = cons[4 * NP + k];
-            L.mat[k] = 0;
-        }
+        const int pp = kp >= 1 && kp <= N ? kp - 1 : blen;   // outside 1..N: a valid byte, discarded
+        const uint8_t *sp = pp < blen ? bef + pp : (pp < blen + ka.Nraw ? raw + (pp - blen) : aft + (pp - blen - ka.Nraw));
+        v_s = *sp;
+        v_up = cons[kp];
+        v_dn = cons[NP + kp];
+        v_pt = cons[2 * NP + kp];
+        v_en = cons[3 * NP + kp];
+        v_fl = cons[4 * NP + kp];
     }
-    bool cst = false;
-    for (int k = 1 + tid; k <= N; k += RG_NT) cst |= (L.flg[k] | L.ptn[k]) != 0;
-    for (int k = tid; k < CT_SIZE; k += RG_NT) L.ct[k] = XS->ctab[k];
-    for (int k = tid; k < 200; k += RG_NT) {
-        L.dt[DT_MMH + k] = (&T.mmH[0][0][0])[k];
-        L.dt[DT_MMI + k] = (&T.mmI[0][0][0])[k];
-        L.dt[DT_MLS + k] = (&T.mlstem[0][0][0])[k];
+    static_assert(RG_NMAX + 2 <= RG_NT, "one position per thread");
+    if (tid < NP) {
+        L.S[tid] = (tid >= 1 && tid <= N) ? v_s : 0;
+        L.up[tid] = v_up;
+        L.dn[tid] = v_dn;
+        L.ptn[tid] = v_pt;
+        L.enc[tid] = v_en;
+        L.flg[tid] = v_fl;
+        L.mat[tid] = 0;
     }
-    for (int k = tid; k < 288; k += RG_NT) L.dt[DT_EXT + k] = (&T.ext[0][0][0])[k];
-    for (int k = tid; k < 8; k += RG_NT) L.dt[DT_TAU + k] = T.termAU[k];
-    for (int k = tid; k <= N; k += RG_NT) L.dt[DT_HP + k] = XS->hp[k];
-    for (int k = tid; k < N + 9; k += RG_NT) L.pw[k] = XS->pwml[k];
-    for (int k = tid; k < MAX_SPECIAL_HP; k += RG_NT) {
-        const bool on = k < XS->n_special;
-        spk[k] = on ? XS->sp_key[k] : 0xFFFFFFFFu;
-        spv[k] = on ? XS->sp_val[k] : 0.f;
+    const bool cst = tid >= 1 && tid <= N && (v_fl | v_pt) != 0;
+#pragma unroll
+    for (int t = 0; t < NCT; t++)
+        if (tid + t * RG_NT < CT_SIZE) L.ct[tid + t * RG_NT] = v_ct[t];
+    if (tid < 200) {
+        L.dt[DT_MMH + tid] = v_mh;
+        L.dt[DT_MMI + tid] = v_mi;
+        L.dt[DT_MLS + tid] = v_ms;
     }
-    for (int k = tid; k < MAX_MOTIF; k += RG_NT) {
-        mcode[k] = XS->motif_code[k];
-        mpt[k] = XS->motif_pt[k];
+    if (tid < 288) L.dt[DT_EXT + tid] = v_ex;
+    if (tid < 8) L.dt[DT_TAU + tid] = v_tau;
+    if (tid <= N) L.dt[DT_HP + tid] = v_hp;
+    if (tid < N + 9) L.pw[tid] = v_pw;
+    if (tid < MAX_SPECIAL_HP) {
+        const bool on = tid < n_sp;
+        spk[tid] = on ? v_spk : 0xFFFFFFFFu;
+        spv[tid] = on ? v_spv : 0.f;
+    }
+    if (tid < MAX_MOTIF) {
+        mcode[tid] = v_mc;
+        mpt[tid] = v_mp;
     }
     for (int k = tid; k < 2 * NP; k += RG_NT) L.mla[k] = 0.f;
     for (int k = C + tid; k < C + RG_SLACK; k += RG_NT) L.qm[k] = L.q1[k] = 0.f;
@@ -549,15 +571,40 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     // slot's diagonal-major tables, one diagonal per wave, lanes = cells; a fold
     // from scratch zeroes qm (spans N-2, N-1 are never computed)
     if (incr) {
-        for (int D = 4 + wid; D <= N - 1; D += RG_NW) {
-            const int od = off(D, N);
-            for (int i = 1 + lane; i <= N - D; i += WAVE) {
-                const float a = src[Cs + od + i - 1], b = src[2 * Cs + od + i - 1];
-                L.qm[rowb(i, N) + D - 4] = a;
-                L.q1[colb(i + D) + i - 1] = b;
+        // this wave's (diagonal, lane-set) items in batches of RB: every load of a
+        // batch in flight before its stores (round 6; a load -> store pair per item
+        // waited on HBM once per item)
+        constexpr int RB = 8;
+        int D = 4 + wid, i0 = 1;
+        const float q5v = src[3 * Cs + min(tid, N)];
+        while (D <= N - 1) {
+            float va[RB], vb[RB];
+            int ia[RB], ib[RB];
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int i = i0 + lane;
+                const bool ok = D <= N - 1 && i <= N - D;
+                const int c = ok ? off(D, N) + i - 1 : 0;
+                va[k] = src[Cs + c];
+                vb[k] = src[2 * Cs + c];
+                ia[k] = ok ? rowb(i, N) + D - 4 : -1;
+                ib[k] = colb(i + D) + i - 1;
+                if (D <= N - 1) {   // next item (uniform)
+                    i0 += WAVE;
+                    if (i0 > N - D) {
+                        D += RG_NW;
+                        i0 = 1;
+                    }
+                }
             }
+#pragma unroll
+            for (int k = 0; k < RB; k++)
+                if (ia[k] >= 0) {
+                    L.qm[ia[k]] = va[k];
+                    L.q1[ib[k]] = vb[k];
+                }
         }
-        for (int k = tid; k <= m_lo - 2 && k <= N; k += RG_NT) L.q5[k] = src[3 * Cs + k];
+        if (tid <= m_lo - 2 && tid <= N) L.q5[tid] = q5v;
     } else {
         for (int k = tid; k < C; k += RG_NT) L.qm[k] = 0.f;
     }
@@ -632,11 +679,10 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
                     if (L.up[i + 1] >= u) {
                         bool special = false;
                         if (u == 3 || u == 4 || u == 6) {
-                            const uint32_t key = hp_key(S, i, u + 2);
-                            for (int q0 = 0; q0 < nsp; q0 += 8) {
-#pragma unroll
-                                for (int t = 0; t < 8; t++)
-                                    if (spk[q0 + t] == key) { h0 = spv[q0 + t]; special = true; }
+                            const int sh = special_hp(spk, hp_key(S, i, u + 2));
+                            if (sh >= 0) {
+                                h0 = spv[sh];
+                                special = true;
                             }
                         }
                         if (!special)
