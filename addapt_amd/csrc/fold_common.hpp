@@ -47,6 +47,28 @@ __device__ __forceinline__ int walker_at(const int *order, const int *mask, int 
     return w;
 }
 
+// A fold workgroup's per-walker words -- its mask, slot index, slot validity and
+// the proposal's changed range -- loaded in one round trip after the walker's index
+// (the chain order -> mask -> slot -> change waited on three); valid is false and
+// c0 < 0 without incremental state.  K: KArgs (dev_types.hpp)
+struct WalkerRef {
+    int w, cur, c0, c1;
+    bool on, valid;
+};
+template <class K>
+__device__ __forceinline__ WalkerRef walker_ref(const K &ka, const int *mask, int wb) {
+    WalkerRef r;
+    r.w = ka.order ? ka.order[wb] : wb;
+    const int w = r.w;
+    const int mk = mask ? mask[w] : 1;
+    r.cur = ka.tab ? int(ka.cur_slot[w]) : 0;
+    r.valid = ka.tab ? ka.tab_valid[w] != 0 : false;
+    r.c0 = ka.chg ? ka.chg[2 * w] : -1;
+    r.c1 = ka.chg ? ka.chg[2 * w + 1] : -1;
+    r.on = mk == 1;
+    return r;
+}
+
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 constexpr int MFE16_FLOOR = -12000;
 // Exactness of the packed 16-bit MFE encoding (kernels.hip MinPlus16): a half

@@ -176,25 +176,27 @@ __device__ __forceinline__ u32 pack2(int lo, int hi) { return (u32(lo) & 0xFFFFu
 
 // One instance per wave (WID): every wave's sweep holds only its own interior-loop
 // block and roles, so the registers of the other waves' roles are not live in it
-template <int NT, int NM, int WID>
-__device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *__restrict__ XS,
-                                              const DevTables *__restrict__ TT, const int *vs, const uint8_t *raw,
-                                              const CP &L, u32 &z, bool &bad, const IncM &inc) {
+// The fold's setup (sequence, tables, refold restore, per-cell pass) and its
+// write-back run in the kernel body, one copy of the code for all eight waves
+// (round 6: as part of the per-wave instances each wave fetched its own copy,
+// ~1.1k instruction-cache misses per fold group, profiles/r06u_icache_pmc.txt).
+// Returns the constrained flag; sst (stamp builds) gets the phase cycles.
+template <int NT, int NM>
+__device__ __forceinline__ bool pair_setup(const KArgs &ka, const DevScaled *__restrict__ XS,
+                                           const DevTables *__restrict__ TT, const int *vs, const uint8_t *raw,
+                                           const CP &L, const IncM &inc, unsigned long long *sst) {
     static_assert(NT == NWV * WAVE, "one wave per block slot");
     const DevVariant V = ka.variants[vs[0]];
     const bool mh0 = ka.variants[vs[0]].motif != 0, mh1 = ka.variants[vs[1]].motif != 0;
     const int N = uni(V.N);
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
-    constexpr int wid = WID;
+    const int wid = uni(tid / WAVE);
     const int NP = L.np;
     const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
 #ifdef ADX_STAMP
     const unsigned long long st_setup0 = __builtin_amdgcn_s_memtime();
 #endif
-    // hairpin length factors of this wave's per-cell-pass diagonals d = 4 + wid + 8m
-    // (lane m; read back by readlane), loaded first so no pass waits on HBM
-    const u32 hpl = __float_as_uint(XS->hp[min(3 + wid + NWV * lane, NMAX)]);
     const bool incr = inc.src != nullptr;
     const int m_lo = uni(inc.m_lo), m_hi = uni(inc.m_hi);
     // changed rows of span dd (cells containing a changed position; mfe_cells.hip)
@@ -219,6 +221,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const u32 v_ms = __float_as_uint((&T0.mlstem[0][0][0])[min(tid, 199)]);
     const u32 v_ex = __float_as_uint((&T0.ext[0][0][0])[min(tid, 287)]);
     const u32 v_tau = __float_as_uint(T0.termAU[tid & 7]);
+    const u32 v_hp = __float_as_uint(XS->hp[min(tid, N)]);   // hairpin length factors (per-cell pass)
     const int ke = min(tid, MFE_E4_SLOTS * 4 - 1);
     const int e4a = MFE_E4_A[ke >> 2][ke & 3], e4u = MFE_E4_U[ke >> 2];
     const int n_sp = XS->n_special;
@@ -270,6 +273,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     }
     if (tid < 288) L.dt[DT_EXT + tid] = v_ex;
     if (tid < 8) L.dt[DT_TAU + tid] = v_tau;
+    u32 *hpf = L.colmin;   // the U slots' space until the sweep (initialised after the per-cell pass)
+    static_assert(4 * (NM + 2) >= NM + 1, "hairpin factors fit the U slots");
+    if (tid <= N) hpf[tid] = v_hp;
     // setup scratch in the partial / split / U slots (first written after the per-cell pass)
     uint32_t *spk = reinterpret_cast<uint32_t *>(L.part);
     u32 *spv = spk + MAX_SPECIAL_HP;
@@ -388,11 +394,8 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     }
     if (tid < MFE_E4_SLOTS * 4) L.e4[tid] = e4a < 0 ? INF16 : v_e4;
     __syncthreads();
-    const u32 mlclosing = __float_as_uint(XS->mlclosing);
-    const u32 mlbase = __float_as_uint(XS->mlbase_sig);
     const u32 mx = __float_as_uint(XS->motif_extra);
     const u32 mextra = (mh0 ? (mx & 0xFFFFu) : 0x7FFFu) | (mh1 ? (mx & 0xFFFF0000u) : 0x7FFF0000u);
-    const int nsp = XS->n_special < MAX_SPECIAL_HP ? XS->n_special : MAX_SPECIAL_HP;
     if (tid == 0) {
         L.q5[0] = 0u;
         for (int j = 1; j <= 4 && j <= N; j++) L.q5[j] = (L.up[j] >= 1) ? L.q5[j - 1] : INF16;
@@ -401,24 +404,63 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     const unsigned long long st_s3 = __builtin_amdgcn_s_memtime();   // motif sites
 #endif
     // ---- per-cell setup (mfe_cells.hip): inner-pair code, hairpin (+ motif) or the
-    // non-pairable mark, multiloop stem of the pairable cells.  Round 6: every
-    // lane-set of two diagonals at once, each in two LDS round trips (the
-    // position words, then the mismatch / stem factors), where the one-cell-at-
-    // a-time loop took ~5 dependent round trips per lane-set
-    auto cell_pass = [&](int dd0) __attribute__((always_inline)) {
-        constexpr int NI = 4;   // items: (dd0, dd0 + NWV) x lane-sets 0, 1
+    // non-pairable mark, multiloop stem of the pairable cells, for the changed band
+    // (a fold from scratch: every cell; a refold restored the others).  Round 6:
+    // the band's rows in quarter-sets of 16 (diagonal d, rows clo(d) + 16c ..), four
+    // quarter-sets per 64-lane item and four items per batch, each batch in two LDS
+    // round trips; items by diagonal left most lanes idle (a refold's band holds
+    // d + 3 rows of diagonal d) and took three times the batches
+    static_assert(NM - 4 <= 2 * WAVE, "the diagonals' quarter-set counts in two lane-sets");
+    int pex[2];   // exclusive prefix of the quarter-set counts of diagonals 4 + x, x = lane + 64 xs
+    int tot = 0;  // quarter-sets
+#pragma unroll
+    for (int xs = 0; xs < 2; xs++) {
+        const int d = 4 + xs * WAVE + lane;
+        const int n = d <= N - 1 ? max(0, chi(d) - clo(d) + 1) : 0;
+        const int q = (n + 15) >> 4;
+        int v = q;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int t = __shfl_up(v, o, WAVE);
+            if (lane >= o) v += t;
+        }
+        pex[xs] = d <= N - 1 ? tot + v - q : 0x7FFFFFFF;
+        tot += __shfl(v, WAVE - 1, WAVE);
+    }
+    tot = uni(tot);
+    // quarter-set k (uniform): the last diagonal whose prefix is <= k, and the row of its first lane
+    auto qmap = [&](int k, int &d, int &i0) __attribute__((always_inline)) {
+        const int c0 = __popcll(__ballot(pex[0] <= k)), c1 = __popcll(__ballot(pex[1] <= k));
+        const int x = uni(c0 + c1 - 1);
+        const int px = x < WAVE ? __builtin_amdgcn_readlane(pex[0], x) : __builtin_amdgcn_readlane(pex[1], x - WAVE);
+        d = 4 + x;
+        i0 = clo(d) + 16 * (k - px);
+    };
+    auto cell_pass = [&](int I0) __attribute__((always_inline)) {
+        constexpr int NI = 4;   // items I0 .. I0 + 3 (quarter-sets 4 I .. 4 I + 3)
         int ii[NI], jj[NI], dv[NI];
         bool ok[NI];
         u32 wim[NI], wi[NI], wi1[NI], wjm[NI], wj[NI], wjp[NI];
         uint32_t mt[NI];
 #pragma unroll
         for (int q = 0; q < NI; q++) {
-            const int d = dd0 + (q >> 1) * NWV;
-            // the changed band's rows (a fold from scratch: every row); a refold
-            // restored the other cells' codes, tables and marks
-            const int r = clo(d) - 1 + lane + (q & 1) * WAVE;
+            int d = 4, r = 0;
+            bool v = false;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int k = 4 * (I0 + q) + g;
+                if (k < tot) {
+                    int dg, ig;
+                    qmap(k, dg, ig);
+                    if ((lane >> 4) == g) {
+                        d = dg;
+                        r = ig + (lane & 15) - 1;
+                        v = r < chi(dg);
+                    }
+                }
+            }
             dv[q] = d;
-            ok[q] = d <= N - 1 && r < chi(d);
+            ok[q] = v;
             const int i = ok[q] ? r + 1 : 1, j = ok[q] ? i + d : 5;
             ii[q] = i;
             jj[q] = j;
@@ -432,10 +474,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
         }
         int ty[NI], ix1[NI];
         bool pr[NI], inb[NI];
-        u32 f1[NI], f2[NI];
+        u32 f1[NI], f2[NI], hv[NI];
 #pragma unroll
         for (int q = 0; q < NI; q++) {
             const int i = ii[q], j = jj[q], d = dv[q];
+            hv[q] = hpf[d - 1];
             const int si = wi[q] & 7, sj = wj[q] & 7;
             ty[q] = ptype(si, sj);
             inb[q] = ok[q];
@@ -456,7 +499,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             L.cc[off(d, N) + i - 1] = static_cast<uint8_t>(rtype(ty[q]) * 25 + (wjp[q] & 7) * 5 + (wim[q] & 7));
             u32 h = INF16;
             if (((wi1[q] >> 8) & 255) >= uint32_t(u)) {
-                h = padd(u32(__builtin_amdgcn_readlane(int(hpl), (d - 4 - wid) / NWV)), f1[q]);
+                h = padd(hv[q], f1[q]);
                 if (u == 3 || u == 4 || u == 6) {   // special hairpins (three diagonals)
                     const int sh = special_hp(spk, hp_key(L.S, i, u + 2));
                     if (sh >= 0) h = spv[sh];
@@ -469,8 +512,7 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
             }
         }
     };
-    static_assert(4 + (WAVE - 1) * NWV > NMAX, "hpl covers every diagonal");
-    for (int dd = 4 + wid; dd <= N - 1; dd += 2 * NWV) cell_pass(dd);
+    for (int I0 = wid * 4; 4 * I0 < tot; I0 += NWV * 4) cell_pass(I0);
 #ifdef ADX_STAMP
     const unsigned long long st_s35 = __builtin_amdgcn_s_memtime();   // this wave's cells (before the barrier)
 #endif
@@ -483,7 +525,40 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     for (int k = tid; k < 6 * NP; k += NT) L.mla[k] = INF16;
     for (int k = tid; k < 4 * NP; k += NT) L.colmin[k] = INF16;
     __syncthreads();
+#ifdef ADX_STAMP
+    {
+        const unsigned long long st_end = __builtin_amdgcn_s_memtime();
+        sst[0] = st_end - st_setup0;
+        sst[1] = st_s1 - st_setup0;
+        sst[2] = st_s2 - st_s1;
+        sst[3] = st_s25 - st_s2;
+        sst[4] = st_s3 - st_s25;
+        sst[5] = st_s4 - st_s3;
+        sst[6] = st_s35 - st_s3;
+    }
+#endif
+    return constrained;
+}
 
+template <int NT, int NM, int WID>
+__device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *__restrict__ XS,
+                                              const DevTables *__restrict__ TT, const int *vs, const CP &L,
+                                              const IncM &inc, const bool constrained, const unsigned long long *sst) {
+    const DevVariant V = ka.variants[vs[0]];
+    const int N = uni(V.N);
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1);
+    constexpr int wid = WID;
+    const int NP = L.np;
+    const u32 *gct = reinterpret_cast<const u32 *>(XS->ctab);
+    const bool incr = inc.src != nullptr;
+    const int m_lo = uni(inc.m_lo), m_hi = uni(inc.m_hi);
+    auto clo = [&](int dd) { return incr ? max(1, m_lo - 1 - dd) : 1; };
+    auto chi = [&](int dd) { return incr ? min(N - dd, m_hi + 1) : N - dd; };
+    auto qlo = [&](int s) { return incr ? max(1, m_lo - 2 - s) : 1; };
+    auto qhi = [&](int s) { return incr ? min(N - s, m_hi + 2) : N - s; };
+    const u32 mlclosing = __float_as_uint(XS->mlclosing);
+    const u32 mlbase = __float_as_uint(XS->mlbase_sig);
     const DevTables &T = *TT;
     const u32 *T11 = reinterpret_cast<const u32 *>(&T.int11[0][0][0][0]);
     const u32 *T21 = reinterpret_cast<const u32 *>(&T.int21[0][0][0][0][0]);
@@ -568,14 +643,17 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
 
 #ifdef ADX_STAMP
     unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long st_last = __builtin_amdgcn_s_memtime();
-    st_acc[8] = st_last - st_setup0;
-    st_acc[11] = st_s1 - st_setup0;
-    st_acc[12] = st_s2 - st_s1;
-    st_acc[13] = st_s25 - st_s2;
-    st_acc[7] = st_s3 - st_s25;
-    st_acc[15] = st_s35 - st_s3;
-    st_acc[14] = st_s4 - st_s3;
+    const unsigned long long st_sw0 = __builtin_amdgcn_s_memtime();
+    unsigned long long st_last = st_sw0;
+    st_acc[11] = sst[1];
+    st_acc[12] = sst[2];
+    st_acc[13] = sst[3];
+    st_acc[7] = sst[4];
+    st_acc[14] = sst[5];
+    st_acc[15] = sst[6];
+#endif
+#ifdef ADX_STAMP
+    st_acc[8] = sst[0] + (st_last - st_sw0);   // setup + the sweep's prelude
 #endif
     int sl = 0;   // list slot of this step: step index % 3
     for (int d = 6; d - 3 <= N; d += 2) {
@@ -1068,6 +1146,14 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     if (lane == 0 && wid < 16)
         for (int k = 0; k < 16; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
 #endif
+}
+
+// the fold's write-back and 16-bit range check (one copy for all waves)
+template <int NT, int NM>
+__device__ __forceinline__ void pair_finish(const KArgs &ka, const int *vs, const CP &L, const IncM &inc, u32 &z,
+                                            bool &bad) {
+    const int N = uni(ka.variants[vs[0]].N);
+    const int tid = threadIdx.x;
     z = L.q5[N];
     if (inc.dst) {   // this fold's tables: the next proposal's unchanged cells
         const size_t C = size_t(ka.cells);
@@ -1100,9 +1186,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
 template <int NT, int NM, int... Ws>
 __device__ __forceinline__ void pair_fold_wave(std::integer_sequence<int, Ws...>, int w, const KArgs &ka,
                                                const DevScaled *__restrict__ XS, const DevTables *__restrict__ TT,
-                                               const int *vs, const uint8_t *seqs, const CP &L, u32 &z, bool &bad,
-                                               const IncM &inc) {
-    ((w == Ws ? (mfe_pair_fold<NT, NM, Ws>(ka, XS, TT, vs, seqs, L, z, bad, inc), 0) : 0), ...);
+                                               const int *vs, const CP &L, const IncM &inc, bool constrained,
+                                               const unsigned long long *sst) {
+    ((w == Ws ? (mfe_pair_fold<NT, NM, Ws>(ka, XS, TT, vs, L, inc, constrained, sst), 0) : 0), ...);
 }
 
 constexpr int MFE_WPE = (2 * NWV + 3) / 4;
@@ -1115,33 +1201,37 @@ mfe_pair_kernel(const KArgs ka, const DevScaled *__restrict__ XS, const DevTable
     const int ng = ka.n_groups2;
     const int wb = int(blockIdx.x) / ng, g = int(blockIdx.x) % ng;
     if (wb >= W) return;
-    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
-    if (w < 0) return;
+    const WalkerRef wr = walker_ref(ka, mask, wb);   // heaviest refolds first
+    if (!wr.on) return;
+    const int w = wr.w;
     if (threadIdx.x < 2) L.flag[threadIdx.x] = 0;
     __syncthreads();
     const int vs[2] = {ka.groups2[2 * g], ka.groups2[2 * g + 1]};
     IncM inc{nullptr, nullptr, 0, 0, nullptr, nullptr};
     if (ka.tab) {
         const size_t Gf = inc_group_floats(ka.cells, ka.Nmax, 1);
-        const int cur = ka.cur_slot[w];
+        const int cur = wr.cur;
         float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
         inc.dst = reinterpret_cast<u32 *>(base + size_t(1 - cur) * ka.tab_slot + size_t(g) * Gf);
         const size_t cco = inc_cc_offset(ka.cells, ka.Nmax, ng, g);
         inc.cc_dst = reinterpret_cast<uint4 *>(base + size_t(1 - cur) * ka.tab_slot + cco);
         // a sibling group may clear tab_valid[w] on overflow while this one reads it:
         // either value is correct (an incremental refold equals a fold from scratch)
-        if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+        if (wr.valid && wr.c0 >= 0) {
             const int lb = ka.variants[vs[0]].before_len;
             inc.src = reinterpret_cast<const u32 *>(base + size_t(cur) * ka.tab_slot + size_t(g) * Gf);
             inc.cc_src = reinterpret_cast<const uint4 *>(base + size_t(cur) * ka.tab_slot + cco);
-            inc.m_lo = ka.chg[2 * w] + 1 + lb;
-            inc.m_hi = ka.chg[2 * w + 1] + 1 + lb;
+            inc.m_lo = wr.c0 + 1 + lb;
+            inc.m_hi = wr.c1 + 1 + lb;
         }
     }
     u32 z = INF16;
     bool bad = false;
-    pair_fold_wave<NT, NM>(std::make_integer_sequence<int, NWV>{}, uni(int(threadIdx.x) / WAVE), ka, XS, TT, vs,
-                           seqs + size_t(w) * ka.Nraw, L, z, bad, inc);
+    unsigned long long sst[7] = {0, 0, 0, 0, 0, 0, 0};
+    const bool constrained = pair_setup<NT, NM>(ka, XS, TT, vs, seqs + size_t(w) * ka.Nraw, L, inc, sst);
+    pair_fold_wave<NT, NM>(std::make_integer_sequence<int, NWV>{}, uni(int(threadIdx.x) / WAVE), ka, XS, TT, vs, L,
+                           inc, constrained, sst);
+    pair_finish<NT, NM>(ka, vs, L, inc, z, bad);
     if (threadIdx.x == 0) {
         const s16x2 q = sv(z);
         const int hv[2] = {q.x, q.y};

@@ -285,7 +285,7 @@ struct PxSizeQ {
 };
 
 #ifdef ADX_STAMP
-__device__ unsigned long long g_stamps_p[16][8];
+__device__ unsigned long long g_stamps_p[16][12];
 #define PSTAMP(k) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_last; st_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #define PX_STP_PARAMS , unsigned long long *st_acc, unsigned long long &st_last
 #define PX_STP_ARGS , st_acc, st_last
@@ -452,10 +452,15 @@ __global__ void __launch_bounds__(PX_NT, 1)
 pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, int W, const int *mask,
                 float *gout) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef ADX_STAMP
+    unsigned long long st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
     const int wb = blockIdx.x / ka.n_groups2, grp = blockIdx.x % ka.n_groups2;
     if (wb >= W) return;
-    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
-    if (w < 0) return;
+    const WalkerRef wr = walker_ref(ka, mask, wb);   // heaviest refolds first
+    if (!wr.on) return;
+    const int w = wr.w;
     const int vs0 = ka.groups2[2 * grp], vs1 = ka.groups2[2 * grp + 1];
     const DevVariant V = ka.variants[vs0];
     const bool hol0 = ka.variants[vs0].motif != 0, hol1 = ka.variants[vs1].motif != 0;
@@ -494,10 +499,6 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
     const int C = Y.C, NP = Y.NP;
     const DevTables &T = *ka.T;
-#ifdef ADX_STAMP
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long st_last = __builtin_amdgcn_s_memtime();
-#endif
 
     // ---- incremental fold state (kernels.hip score_sequence / Inc): this group's
     // tables of the current sequence (src) and the proposal's (dst)
@@ -508,16 +509,16 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     uint4 *cc_dst = nullptr;
     int m_lo = 0, m_hi = 0;
     if (ka.tab) {
-        const int cur = ka.cur_slot[w];
+        const int cur = wr.cur;
         float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
         dst = base + size_t(1 - cur) * ka.tab_slot + size_t(grp) * 2 * B1;
         const size_t cco = inc_cc_offset_pf(ka.cells, ka.Nmax, ka.n_groups2, grp);
         cc_dst = reinterpret_cast<uint4 *>(base + size_t(1 - cur) * ka.tab_slot + cco);
-        if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+        if (wr.valid && wr.c0 >= 0) {
             src = base + size_t(cur) * ka.tab_slot + size_t(grp) * 2 * B1;
             cc_src = reinterpret_cast<const uint4 *>(base + size_t(cur) * ka.tab_slot + cco);
-            m_lo = ka.chg[2 * w] + 1 + V.before_len;
-            m_hi = ka.chg[2 * w + 1] + 1 + V.before_len;
+            m_lo = wr.c0 + 1 + V.before_len;
+            m_hi = wr.c1 + 1 + V.before_len;
         }
     }
     const bool incr = src != nullptr;
@@ -529,6 +530,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     auto qlo = [&](int sq) { return incr ? max(1, m_lo - 2 - sq) : 1; };
     auto qhi = [&](int sq) { return incr ? min(N - sq, m_hi + 2) : N - sq; };
 
+    PSTAMP(8);   // the prologue (walker, slot, variant words)
     // ---- setup loads (round 6): the one element of every table and of the sequence /
     // constraint arrays this thread stores, all in flight at once and stored before
     // the restore's loads are issued (a loop per table waited on each load in turn, the
@@ -599,6 +601,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         mcode[tid] = v_mc;
         mpt[tid] = v_mp;
     }
+    PSTAMP(9);   // setup loads and stores
     // ---- refold restore: every table from the current slot (the changed cells are
     // recomputed over it), two cells per lane and load, both folds interleaved.
     // The loads are issued here and stored to LDS after the motif scan, so their
@@ -632,6 +635,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     }
     for (int k = tid; k < 2 * NP; k += PX_NT) L.mla[k] = f2{0.f, 0.f};
     for (int k = C + tid; k < C + PX_SLACK; k += PX_NT) L.qb[k] = L.qm[k] = L.q1[k] = f2{0.f, 0.f};
+    PSTAMP(10);   // the restore's loads issued
     __syncthreads();   // orders tid 0's zeroing of the block_or word before the ORs
     const bool constrained = block_or(reinterpret_cast<int *>(smem + Y.FL), cst);
     PSTAMP(1);
@@ -1058,7 +1062,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     }
 #ifdef ADX_STAMP
     if (lane == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
+        for (int k = 0; k < 12; k++) atomicAdd(&g_stamps_p[wid][k], st_acc[k]);
 #endif
     __syncthreads();
     // ---- the proposal's tables (the next step's unchanged cells) and the energies
@@ -1113,10 +1117,10 @@ hipError_t launch_pf_cells(const KArgs &ka, const uint8_t *seqs, int W, const in
 }  // namespace adx
 
 #ifdef ADX_STAMP
-extern "C" int adx_debug_stamps_pf(unsigned long long *out, int reset) {  // [16][8]
+extern "C" int adx_debug_stamps_pf(unsigned long long *out, int reset) {  // [16][12]
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(adx::g_stamps_p), sizeof(adx::g_stamps_p)) != hipSuccess) return 1;
     if (reset) {
-        static unsigned long long z[16][8] = {};
+        static unsigned long long z[16][12] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(adx::g_stamps_p), z, sizeof(z)) != hipSuccess) return 2;
     }
     return 0;

@@ -384,8 +384,9 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     const int wb = blockIdx.x / ng, rem = blockIdx.x % ng;
     const int grp = rem >> 1, half = rem & 1;
     if (wb >= W) return;
-    const int w = walker_at(ka.order, mask, wb);   // heaviest refolds first
-    if (w < 0) return;
+    const WalkerRef wr = walker_ref(ka, mask, wb);   // heaviest refolds first
+    if (!wr.on) return;
+    const int w = wr.w;
     const int v0 = ka.groups2[2 * grp], vh = ka.groups2[2 * grp + half];
     if (half == 1 && vh == v0) return;   // a lone variant: one fold
     const DevVariant V = ka.variants[vh];
@@ -444,13 +445,13 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     float *dst = nullptr;
     int m_lo = 0, m_hi = 0;
     if (ka.tab) {
-        const int cur = ka.cur_slot[w];
+        const int cur = wr.cur;
         float *base = ka.tab + size_t(w) * 2 * ka.tab_slot;
         dst = base + size_t(1 - cur) * ka.tab_slot + size_t(grp) * 2 * B1 + size_t(half) * B1;
-        if (ka.tab_valid[w] && ka.chg && ka.chg[2 * w] >= 0) {
+        if (wr.valid && wr.c0 >= 0) {
             src = base + size_t(cur) * ka.tab_slot + size_t(grp) * 2 * B1 + size_t(half) * B1;
-            m_lo = ka.chg[2 * w] + 1 + V.before_len;
-            m_hi = ka.chg[2 * w + 1] + 1 + V.before_len;
+            m_lo = wr.c0 + 1 + V.before_len;
+            m_hi = wr.c1 + 1 + V.before_len;
         }
     }
     // qb of every cell, read back by Q: the slot, or this workgroup's scratch
@@ -621,9 +622,9 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     for (int D = 4 + wid; D <= N - 1; D += RG_NW) {
         const int od = off(D, N), lo = clo(D), hi = chi(D);
         int base = 0;
-        for (int i0 = 1; i0 <= N - D; i0 += WAVE) {
+        for (int i0 = lo; i0 <= hi; i0 += WAVE) {   // the changed band's rows (round 6: every row before)
             const int i = i0 + lane;
-            const bool inb = i <= N - D && i >= lo && i <= hi;
+            const bool inb = i <= hi;
             bool pr = false;
             if (inb) {
                 const int j = i + D;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave phase breakdown of pf_cells_kernel (diagnostic stamp build:
 ADX_LIB=addapt_amd/_lib/ablate/lib_stamp.so).  Runs PF MC steps (N=100 bench
-objective).  Waves 0-7 = B (interior loops), 8-9 M, 10-11 F, 12 Q, 13 records.
+objective; "tables" = the barrier + block_or after s.prolog, s.loads, s.rissue).  Waves 0-7 = B (interior loops), 8-9 M, 10-11 F, 12 Q, 13 records.
 usage: pf_cells_stamps.py [N] [W] [steps]"""
 import ctypes as C
 import os
@@ -22,15 +22,15 @@ eng = native.Engine(tmpl, [active], workloads.default_objective(), aptamer=apt,
 seqs = workloads.walker_sequences(tmpl, [active], W)
 eng.walkers_init(list(range(W)), seqs)
 eng.run_steps(1)
-buf = (C.c_ulonglong * 128)()
+buf = (C.c_ulonglong * 192)()
 L.adx_debug_stamps_pf(buf, 1)
 eng.run_steps(steps)
 L.adx_debug_stamps_pf(buf, 1)
 _, _, c = eng.download()
 scored = W * steps * float(c[:, 0].sum() + c[:, 1].sum() + c[:, 3].sum()) / max(1, c.sum())
 G = scored * max(1, eng.info.n_variants // 2)   # workgroups: one per (walker, apo/holo group)
-cols = ["cellpass", "tables", "Bcell", "Bshape", "work", "Bwrite", "barrier", "restore"]
+cols = ["cellpass", "tables", "Bcell", "Bshape", "work", "Bwrite", "barrier", "restore", "s.prolog", "s.loads", "s.rissue"]
 print("cycles per workgroup per wave (N=%d, W=%d, %d steps, %.1f workgroups)" % (N, W, steps, G))
 print("wave " + " ".join("%9s" % n for n in cols))
 for w in range(16):
-    print("%4d " % w + " ".join("%9d" % (buf[w * 8 + k] // max(1, G)) for k in range(8)))
+    print("%4d " % w + " ".join("%9d" % (buf[w * 12 + k] // max(1, G)) for k in range(11)))
