@@ -393,6 +393,29 @@ __device__ __forceinline__ bool pair_setup(const KArgs &ka, const DevScaled *__r
         if (tid <= m_lo - 2 && tid <= N) L.q5[tid] = r5;
     }
     if (tid < MFE_E4_SLOTS * 4) L.e4[tid] = e4a < 0 ? INF16 : v_e4;
+    // the per-cell pass's quarter-sets (below): diagonal d's band rows in sets of 16,
+    // listed diagonal by diagonal in the split slots' space (free until the sweep)
+    // by the waves of lane-sets 0, 1 of the diagonals: qtab[k] = d | first row << 8
+    static_assert(NM - 4 <= 2 * WAVE, "the diagonals' quarter-set counts in two lane-sets");
+    static_assert((NM - 4) + ((NM - 4) * (NM - 3) / 2 + 15) / 16 <= 6 * (NM + 2), "quarter-sets fit the split slots");
+    u32 *qtab = L.mla;
+    int tot = 0;  // quarter-sets
+#pragma unroll
+    for (int xs = 0; xs < 2; xs++) {
+        const int d = 4 + xs * WAVE + lane;
+        const int n = d <= N - 1 ? max(0, chi(d) - clo(d) + 1) : 0;
+        const int q = (n + 15) >> 4;
+        int v = q;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int t = __shfl_up(v, o, WAVE);
+            if (lane >= o) v += t;
+        }
+        if (wid == xs)
+            for (int c = 0; c < q; c++) qtab[tot + v - q + c] = u32(d) | (u32(clo(d) + 16 * c) << 8);
+        tot += __shfl(v, WAVE - 1, WAVE);
+    }
+    tot = uni(tot);
     __syncthreads();
     const u32 mx = __float_as_uint(XS->motif_extra);
     const u32 mextra = (mh0 ? (mx & 0xFFFFu) : 0x7FFFu) | (mh1 ? (mx & 0xFFFF0000u) : 0x7FFF0000u);
@@ -410,55 +433,19 @@ __device__ __forceinline__ bool pair_setup(const KArgs &ka, const DevScaled *__r
     // quarter-sets per 64-lane item and four items per batch, each batch in two LDS
     // round trips; items by diagonal left most lanes idle (a refold's band holds
     // d + 3 rows of diagonal d) and took three times the batches
-    static_assert(NM - 4 <= 2 * WAVE, "the diagonals' quarter-set counts in two lane-sets");
-    int pex[2];   // exclusive prefix of the quarter-set counts of diagonals 4 + x, x = lane + 64 xs
-    int tot = 0;  // quarter-sets
-#pragma unroll
-    for (int xs = 0; xs < 2; xs++) {
-        const int d = 4 + xs * WAVE + lane;
-        const int n = d <= N - 1 ? max(0, chi(d) - clo(d) + 1) : 0;
-        const int q = (n + 15) >> 4;
-        int v = q;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const int t = __shfl_up(v, o, WAVE);
-            if (lane >= o) v += t;
-        }
-        pex[xs] = d <= N - 1 ? tot + v - q : 0x7FFFFFFF;
-        tot += __shfl(v, WAVE - 1, WAVE);
-    }
-    tot = uni(tot);
-    // quarter-set k (uniform): the last diagonal whose prefix is <= k, and the row of its first lane
-    auto qmap = [&](int k, int &d, int &i0) __attribute__((always_inline)) {
-        const int c0 = __popcll(__ballot(pex[0] <= k)), c1 = __popcll(__ballot(pex[1] <= k));
-        const int x = uni(c0 + c1 - 1);
-        const int px = x < WAVE ? __builtin_amdgcn_readlane(pex[0], x) : __builtin_amdgcn_readlane(pex[1], x - WAVE);
-        d = 4 + x;
-        i0 = clo(d) + 16 * (k - px);
-    };
     auto cell_pass = [&](int I0) __attribute__((always_inline)) {
-        constexpr int NI = 4;   // items I0 .. I0 + 3 (quarter-sets 4 I .. 4 I + 3)
+        constexpr int NI = 4;   // items I0 .. I0 + 3 (quarter-sets 4 I .. 4 I + 3, lanes 16 g ..)
         int ii[NI], jj[NI], dv[NI];
         bool ok[NI];
         u32 wim[NI], wi[NI], wi1[NI], wjm[NI], wj[NI], wjp[NI];
         uint32_t mt[NI];
 #pragma unroll
         for (int q = 0; q < NI; q++) {
-            int d = 4, r = 0;
-            bool v = false;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const int k = 4 * (I0 + q) + g;
-                if (k < tot) {
-                    int dg, ig;
-                    qmap(k, dg, ig);
-                    if ((lane >> 4) == g) {
-                        d = dg;
-                        r = ig + (lane & 15) - 1;
-                        v = r < chi(dg);
-                    }
-                }
-            }
+            const int k = 4 * (I0 + q) + (lane >> 4);   // the lane's quarter-set
+            const u32 e = qtab[k < tot ? k : 0];
+            const int d = k < tot ? int(e & 255) : 4;
+            const int r = int(e >> 8) + (lane & 15) - 1;
+            const bool v = k < tot && r < chi(d);
             dv[q] = d;
             ok[q] = v;
             const int i = ok[q] ? r + 1 : 1, j = ok[q] ? i + d : 5;
