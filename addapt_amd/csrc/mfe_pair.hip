@@ -62,7 +62,10 @@ namespace {
 // waves land 3, 3, 2, 2 on the SIMDs, so a second one does not fit at 96 VGPRs)
 constexpr int NWV = 8;
 constexpr int F_WAVE = 7;
-constexpr int PRIO_ROLE = 2;   // s_setprio of the one-wave roles over the block waves
+#ifndef ADX_PRIO_ROLE
+#define ADX_PRIO_ROLE 2
+#endif
+constexpr int PRIO_ROLE = ADX_PRIO_ROLE;   // s_setprio of the one-wave roles over the block waves
 
 // (A/B round 6: a block on the finalize wave too, ADX_GEN_PAIR_NBLK=8, measured
 // -5.7 %: the finalize wave then sets the step; nine block waves in ten -37 %)

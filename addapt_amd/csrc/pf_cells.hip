@@ -56,6 +56,9 @@ __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most ite
          : (w >= PX_M0 + 4 && w < PX_NW) ? w - PX_M0 : -1;
 }
 constexpr int PX_NMAX = 100;
+#ifndef PX_ROLE_PRIO
+#define PX_ROLE_PRIO 2   // s_setprio of the role waves (M, F, Q, R) over the interior-loop waves
+#endif
 constexpr int PX_RF = 8;              // record fields (rec_store): word, mmo, mo, m23, 1x1..2x2 factors
 constexpr int PX_SLACK = 16;
 
@@ -919,7 +922,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
     } else {
         // the M / F / Q / R chains set the step time; issue arbitration favours the
         // older (B) waves of the workgroup, so these run at a higher priority
-        __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(PX_ROLE_PRIO);
         // one sweep instance per role (round 6): each holds only its own role's
         // registers (the shared loop kept every role's values live: 38 SGPR spills)
         auto sweep = [&](auto role_c) __attribute__((always_inline)) {
