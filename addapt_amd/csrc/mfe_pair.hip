@@ -635,9 +635,11 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
     unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long st_sw0 = __builtin_amdgcn_s_memtime();
     unsigned long long st_last = st_sw0;
+#ifndef ADX_STAMP_F
     st_acc[11] = sst[1];
     st_acc[12] = sst[2];
     st_acc[13] = sst[3];
+#endif
     st_acc[7] = sst[4];
     st_acc[14] = sst[5];
     st_acc[15] = sst[6];
@@ -751,6 +753,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                           [aUj] "v"(aU + uint32_t(jA)), [aDj] "v"(aD + uint32_t(jA - 1))
                         : "memory");
                 }
+#ifdef ADX_STAMP_F
+                PSTAMP(11);   // F: the read batch
+#endif
                 static_assert(NM + 2 == PLay<NM>::NP, "partial halves are NP words apart");
                 // the loop-correction factors of the stack / bulge-1 shapes and the cells' own terms
                 const int tyA = ptype(si, sj), tyB = ptype(si, sjp);
@@ -809,6 +814,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                     q1B = pfin(f1);
                     if (own) L.qm1[cmB] = q1B;
                 }
+#ifdef ADX_STAMP_F
+                PSTAMP(12);   // F: the cells' terms
+#endif
                 // U of row i+1 in column jA+1 (span e0) is the next lane's cell A
                 const u32 UA1 = u32(__builtin_amdgcn_ds_bpermute((lane + 1) * 4, int(UA)));
                 const u32 UB = ui >= 1 ? pmin(q1B, padd(UA1, mlbase)) : q1B;
@@ -827,6 +835,9 @@ __device__ __forceinline__ void mfe_pair_fold(const KArgs &ka, const DevScaled *
                         L.qm[rowb(i, N) + e1 - 4] = pfin(pmin(e1 >= 9 ? spB : INF16, UB));
                 }
                 __builtin_amdgcn_s_setprio(0);
+#ifdef ADX_STAMP_F
+                PSTAMP(13);   // F: U, the stores
+#endif
             }
         }
         PSTAMP(2);
