@@ -56,6 +56,9 @@ __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most ite
          : (w >= PX_M0 + 4 && w < PX_NW) ? w - PX_M0 : -1;
 }
 constexpr int PX_NMAX = 100;
+#ifndef PX_PART
+#define PX_PART 4   // interior-loop size partition of the eight blocks (pf_cells_kernel; 0: before r07g)
+#endif
 #ifndef PX_ROLE_PRIO
 #define PX_ROLE_PRIO 2   // s_setprio of the role waves (M, F, Q, R) over the interior-loop waves
 #endif
@@ -896,13 +899,60 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         // stamps showed busiest (profiles/r06e_pf_cells_stamps.txt) on an eighth wave
         switch (wid) {
             case 0: pb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#if PX_PART != 5
             case 1: pb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
+#if PX_PART != 7
             case 2: pb_sweep<3, 20, 18, 8, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
+#if PX_PART == 1   // (A/B knobs) size 16 from block 4 to block 3
+            case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 2   // size 16 from block 4 to block 5
+            case 3: pb_sweep<28, 26, 1, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 16, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 3   // size 0 from block 4 to block 3
+            case 3: pb_sweep<28, 26, 1, 7, 0>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 16, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 5   // as 4, and size 0 from block 4 to block 1
+            case 1: pb_sweep<4, 21, 19, 10, 0>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, -1, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 6   // size 16 from block 4 to block 5, size 15 from block 6 to block 3
+            case 3: pb_sweep<28, 26, 1, 7, 15>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 16, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 7   // as 4, and size 13 from block 7 to block 2
+            case 2: pb_sweep<3, 20, 18, 8, 13>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 4   // size 16 from block 4 to block 3, size 15 from block 6 to block 5
+            case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#else
             case 3: pb_sweep<28, 26, 1, 7, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 4: pb_sweep<29, 27, 16, 0, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
+#if PX_PART == 7
+            default: pb_sweep<9, 14, 6, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#else
             default: pb_sweep<9, 14, 6, 13, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
         }
 #else
         switch (wid) {
