@@ -62,6 +62,9 @@ namespace adx {
 namespace {
 
 constexpr int OX_NMAX = 112;
+#ifndef OX_PART
+#define OX_PART 0   // interior-loop size partition of the B waves (A/B knob)
+#endif
 constexpr int OX_SLACK = 64;          // zeroed floats after each cell table (reads past a row end)
 
 // LDS carve for folded length N (runtime; the host sizes the launch with it)
@@ -545,10 +548,27 @@ outside_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *
             case 3: b_sweep<2, 3, 30, 6, 11, -1>(L, N, lane, std::integral_constant<int, 3>{}, fin OX_STP_ARGS); break;
             case 4: b_sweep<2, 29, 28, 27, 1, -1>(L, N, lane, std::integral_constant<int, 4>{}, fin OX_STP_ARGS); break;
             case 5: b_sweep<2, 26, 25, 24, 2, -1>(L, N, lane, std::integral_constant<int, 5>{}, fin OX_STP_ARGS); break;
+#if OX_PART == 1   // (A/B knobs) size 10 from block 8 to the record wave 7, size 9 from block 9 to block 6
+            case 6: b_sweep<2, 22, 21, 20, 8, 9>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
+            case 7: b_sweep<2, 10, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;
+            case 8: b_sweep<2, 18, 17, 16, -1, -1>(L, N, lane, std::integral_constant<int, 8>{}, fin OX_STP_ARGS); break;
+            default: b_sweep<2, 14, 13, 12, -1, -1>(L, N, lane, std::integral_constant<int, 9>{}, fin OX_STP_ARGS); break;   // wave 9
+#elif OX_PART == 2   // size 10 from block 8 to the record wave 7
+            case 6: b_sweep<2, 22, 21, 20, 8, -1>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
+            case 7: b_sweep<2, 10, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;
+            case 8: b_sweep<2, 18, 17, 16, -1, -1>(L, N, lane, std::integral_constant<int, 8>{}, fin OX_STP_ARGS); break;
+            default: b_sweep<2, 14, 13, 12, 9, -1>(L, N, lane, std::integral_constant<int, 9>{}, fin OX_STP_ARGS); break;   // wave 9
+#elif OX_PART == 3   // size 10 from block 8 to block 6
+            case 6: b_sweep<2, 22, 21, 20, 8, 10>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
+            case 7: b_sweep<2, -1, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;
+            case 8: b_sweep<2, 18, 17, 16, -1, -1>(L, N, lane, std::integral_constant<int, 8>{}, fin OX_STP_ARGS); break;
+            default: b_sweep<2, 14, 13, 12, 9, -1>(L, N, lane, std::integral_constant<int, 9>{}, fin OX_STP_ARGS); break;   // wave 9
+#else
             case 6: b_sweep<2, 22, 21, 20, 8, -1>(L, N, lane, std::integral_constant<int, 6>{}, fin OX_STP_ARGS); break;
             case 7: b_sweep<2, -1, -1, -1, -1, -1>(L, N, lane, std::integral_constant<int, 7>{}, fin OX_STP_ARGS); break;
             case 8: b_sweep<2, 18, 17, 16, 10, -1>(L, N, lane, std::integral_constant<int, 8>{}, fin OX_STP_ARGS); break;
             default: b_sweep<2, 14, 13, 12, 9, -1>(L, N, lane, std::integral_constant<int, 9>{}, fin OX_STP_ARGS); break;   // wave 9
+#endif
         }
     } else for (int d = N - 1; d >= 3; d--) {
         const int nls = d >= 4 ? (N - d + WAVE - 1) / WAVE : 0;   // lane-sets of diagonal d
