@@ -57,7 +57,7 @@ __host__ __device__ constexpr int px_mw(int w) {   // M wave index (0 = most ite
 }
 constexpr int PX_NMAX = 100;
 #ifndef PX_PART
-#define PX_PART 4   // interior-loop size partition of the eight blocks (pf_cells_kernel; 0: before r07g)
+#define PX_PART 8   // interior-loop size partition of the eight blocks (pf_cells_kernel; 0: before r07g, A/B r07g-r07i)
 #endif
 #ifndef PX_ROLE_PRIO
 #define PX_ROLE_PRIO 2   // s_setprio of the role waves (M, F, Q, R) over the interior-loop waves
