@@ -43,6 +43,9 @@ namespace adx {
 namespace {
 
 constexpr int RG_NW = 14;
+#ifndef RG_PART
+#define RG_PART 0   // interior-loop size partition of the seven blocks (A/B knob)
+#endif
 constexpr int RG_NT = RG_NW * WAVE;
 constexpr int RG_NB = 7;              // interior-loop blocks (waves 0..6)
 constexpr int RG_NMW = 4;             // qm item waves
@@ -841,13 +844,32 @@ pf_ring_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs, 
     RSTAMP(0);   // setup
     if (wid < RG_NB) {
         switch (wid) {
+            // (A/B knob RG_PART: sizes moved off block 4, the busiest in the stamps,
+            // profiles/r06u_pf_ring_stamps.txt)
+#if RG_PART == 1   // 13 -> block 0, 0 -> block 1
+            case 0: rb_sweep<5, 22, 12, 11, 13>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 1: rb_sweep<4, 21, 19, 10, 0>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 4: rb_sweep<29, 27, 16, -1, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+#elif RG_PART == 2   // 16 -> block 0
+            case 0: rb_sweep<5, 22, 12, 11, 16>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 1: rb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 4: rb_sweep<29, 27, 13, 0, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+#elif RG_PART == 3   // 13 -> block 6, 0 -> block 1
+            case 0: rb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 1: rb_sweep<4, 21, 19, 10, 0>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 4: rb_sweep<29, 27, 16, -1, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            default: rb_sweep<24, 25, 23, 15, 13>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+#else
             case 0: rb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
             case 1: rb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            case 4: rb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
+#endif
             case 2: rb_sweep<3, 20, 18, 8, 6>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
             case 3: rb_sweep<28, 26, 1, 9, 7>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
-            case 4: rb_sweep<29, 27, 16, 13, 0>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
             case 5: rb_sweep<30, 2, 17, 14, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
-            default: rb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end RG_STP_ARGS); break;
         }
     } else {
         __builtin_amdgcn_s_setprio(2);
