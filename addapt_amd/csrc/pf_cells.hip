@@ -899,10 +899,10 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
         // stamps showed busiest (profiles/r06e_pf_cells_stamps.txt) on an eighth wave
         switch (wid) {
             case 0: pb_sweep<5, 22, 12, 11, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
-#if PX_PART != 5 && PX_PART != 8
+#if PX_PART != 5 && PX_PART < 8
             case 1: pb_sweep<4, 21, 19, 10, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
 #endif
-#if PX_PART != 7 && PX_PART != 8
+#if PX_PART != 7 && PX_PART < 8
             case 2: pb_sweep<3, 20, 18, 8, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
 #endif
 #if PX_PART == 1   // (A/B knobs) size 16 from block 4 to block 3
@@ -944,6 +944,25 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             case 4: pb_sweep<29, 27, -1, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 5: pb_sweep<30, 2, 17, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 9 || PX_PART == 10 || PX_PART == 11   // as 8, then 8 (9, 11) from block 2 and 15 (10, 11) from block 5 to block 4
+            case 1: pb_sweep<4, 21, 19, 10, 0>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#if PX_PART == 10
+            case 2: pb_sweep<3, 20, 18, 8, 13>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#else
+            case 2: pb_sweep<3, 20, 18, 13, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
+            case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#if PX_PART == 9
+            case 4: pb_sweep<29, 27, 8, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#elif PX_PART == 10
+            case 4: pb_sweep<29, 27, 15, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#else
+            case 4: pb_sweep<29, 27, 8, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+            case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
+#endif
+            case 6: pb_sweep<24, 25, 23, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
 #elif PX_PART == 4   // size 16 from block 4 to block 3, size 15 from block 6 to block 5
             case 3: pb_sweep<28, 26, 1, 7, 16>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 4: pb_sweep<29, 27, 0, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
@@ -955,7 +974,7 @@ pf_cells_kernel(KArgs ka, const DevScaled *__restrict__ XS, const uint8_t *seqs,
             case 5: pb_sweep<30, 2, 17, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
             case 6: pb_sweep<24, 25, 23, 15, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
 #endif
-#if PX_PART == 7 || PX_PART == 8
+#if PX_PART == 7 || PX_PART >= 8
             default: pb_sweep<9, 14, 6, -1, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
 #else
             default: pb_sweep<9, 14, 6, 13, -1>(L, XS, N, lane, wid, constrained, s_end PX_STP_ARGS); break;
